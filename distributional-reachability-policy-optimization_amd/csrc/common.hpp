@@ -1,0 +1,226 @@
+// Shared device/host helpers for libdrpo_hip (gfx950 / CDNA4 only).
+//
+//  * C-ABI error plumbing (thread-local last-error string, DRPO_* return codes)
+//  * Philox4x32-10 counter RNG + Box-Muller (production-mode noise; parity mode
+//    reads caller-provided noise instead)
+//  * tile_dense<>: one MLP layer for a 16/32-row tile held in LDS, computed with
+//    the exact-fp32 MFMA v_mfma_f32_16x16x4_f32 by a 256-thread workgroup
+//    (4 wave64s, waves split the output columns into 16-wide blocks).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#define DRPO_API extern "C" __attribute__((visibility("default")))
+
+enum DrpoStatus { DRPO_OK = 0, DRPO_EINVAL = 1, DRPO_EHIP = 2, DRPO_EUNSUPPORTED = 3 };
+
+void drpo_set_error(const char* fmt, ...);
+
+#define DRPO_REQUIRE(cond, ...)             \
+  do {                                      \
+    if (!(cond)) {                          \
+      drpo_set_error(__VA_ARGS__);          \
+      return DRPO_EINVAL;                   \
+    }                                       \
+  } while (0)
+
+#define DRPO_LAUNCH_CHECK(name)                                               \
+  do {                                                                        \
+    hipError_t _e = hipGetLastError();                                        \
+    if (_e != hipSuccess) {                                                   \
+      drpo_set_error("%s launch failed: %s", name, hipGetErrorString(_e));    \
+      return DRPO_EHIP;                                                       \
+    }                                                                         \
+  } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace drpo {
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_TANH = 3 };
+
+constexpr int WG = 256;     // threads per workgroup (4 x wave64)
+
+__host__ __device__ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// LDS row stride (floats) for an activation tile of width K: K rounded up to a
+// multiple of 64, +8. Row stride == 8 (mod 64) dwords makes the 16x16x4 A-fragment
+// ds_read_b128 pattern (rows l&15, k-offset 4*(l>>4)) bank-conflict free.
+__host__ __device__ inline int lds_ld(int K) { return round_up(K, 64) + 8; }
+
+template <int ACT>
+__device__ __forceinline__ float act_fn(float x) {
+  if constexpr (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
+  else if constexpr (ACT == ACT_SILU) return x / (1.f + expf(-x));
+  else if constexpr (ACT == ACT_TANH) return tanhf(x);
+  else return x;
+}
+
+// torch softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplusf(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float u32_to_unit(uint32_t v) {   // (0, 1]
+  return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// 4 standard normals for (stream, counter words)
+__device__ __forceinline__ void philox_normal4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
+                                               uint32_t c3, float out[4]) {
+  u32x4 r = philox({c0, c1, c2, c3}, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float u1 = u32_to_unit(r.x), u2 = u32_to_unit(r.y), u3 = u32_to_unit(r.z), u4 = u32_to_unit(r.w);
+  float m1 = sqrtf(-2.f * logf(u1)), m2 = sqrtf(-2.f * logf(u3));
+  float s1, c1f, s2, c2f;
+  sincosf(6.28318530718f * u2, &s1, &c1f);
+  sincosf(6.28318530718f * u4, &s2, &c2f);
+  out[0] = m1 * c1f; out[1] = m1 * s1; out[2] = m2 * c2f; out[3] = m2 * s2;
+}
+
+// ---------------------------------------------------------------------------
+// tile_dense: out[r][c] = act(sum_k in[r][k] * W[c*ldw + k] + b[c]) for a tile of
+// RB*16 rows. `in` / `out` are LDS tiles with row strides ldi / ldo; columns
+// [N, round_up(N,16)) of `out` are written as 0 so the next layer can read a
+// zero-padded K. W is row-major [N][ldw] (PyTorch Linear layout) in global
+// memory (L2-resident: every workgroup streams the same weights).
+//
+// MFMA 16x16x4 f32 mapping (CDNA4): lane l supplies A[row=l&15][k=l>>4] and
+// B[k=l>>4][col=l&15]; D[row=4*(l>>4)+r][col=l&15] in acc[r]. A k-chunk of 16 is
+// fed as 4 MFMAs where lane group g=l>>4 supplies k = k0+4g+m for MFMA m, so
+// both operands are loaded as one float4 per lane (A: ds_read_b128 from LDS,
+// B: one 16-byte global load of 4 consecutive W[col][k]).
+// ---------------------------------------------------------------------------
+template <int RB, int MAXC>
+struct DenseFrag {
+  f32x4 acc[RB][MAXC];
+};
+
+// Branch-free weight-fragment load. The address is clamped into the matrix and
+// NO mask is applied: k >= K lanes multiply zero-padded activation columns (every
+// LDS tile is zero beyond its width up to the next multiple of 16) and columns
+// j >= N are discarded by the epilogue, so the (finite) clamped values never reach
+// an output. With no control flow around the loads the compiler keeps several
+// k-steps in flight with counted vmcnt waits.
+template <bool VEC>
+__device__ __forceinline__ f32x4 load_w4(const float* __restrict__ W, int ldw, int j, int kk, int N, int K) {
+  const float* row = W + (size_t)(j < N ? j : N - 1) * ldw;
+  if constexpr (VEC) {   // K % 4 == 0, rows 16-byte aligned
+    return *reinterpret_cast<const f32x4*>(row + (kk < K ? kk : K - 4));
+  } else {
+    f32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = row[kk + i < K ? kk + i : K - 1];
+    return r;
+  }
+}
+
+// Weight fragments are streamed through a static register ring of depth PF_D:
+// the loads for k-step s+PF_D-1 are issued while k-step s computes, so up to
+// PF_D-1 k-steps (each >= 4*MAXC*RB MFMAs) of L2 latency are hidden even at one
+// wave per SIMD. The ring is indexed only by compile-time constants (unrolled),
+// so it stays in VGPRs.
+constexpr int PF_D = 4;
+
+template <int RB, int MAXC, int ACT, bool VEC>
+__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
+                                                const float* __restrict__ bias, int N, float* out, int ldo) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NB = (N + 15) >> 4;
+
+  f32x4 acc[RB][MAXC];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 bq[PF_D][MAXC];
+#pragma unroll
+  for (int u = 0; u < PF_D - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int cb = wave + 4 * c;
+      bq[u][c] = load_w4<VEC>(W, ldw, cb * 16 + l15, 16 * u + 4 * g, N, K);
+    }
+  for (int kb = 0; kb < K; kb += 16 * PF_D) {
+#pragma unroll
+    for (int u = 0; u < PF_D; ++u) {
+      const int k0 = kb + 16 * u;
+      const int kl = k0 + 16 * (PF_D - 1);
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        const int cb = wave + 4 * c;
+        bq[(u + PF_D - 1) % PF_D][c] = load_w4<VEC>(W, ldw, cb * 16 + l15, kl + 4 * g, N, K);
+      }
+      if (k0 < K) {
+        f32x4 a[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          a[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int c = 0; c < MAXC; ++c)   // out-of-range column blocks compute discarded values
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+              acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][m], bq[u][c][m], acc[rb][c], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int cb = wave + 4 * c;
+    if (cb >= NB) continue;
+    const int col = cb * 16 + l15;
+    const float bv = (col < N && bias) ? bias[col] : 0.f;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * 16 + 4 * g + r;
+        out[row * ldo + col] = (col < N) ? act_fn<ACT>(acc[rb][c][r] + bv) : 0.f;
+      }
+  }
+}
+
+// Row-aligned fast path (float4 weight loads) when K % 4 == 0, else scalar loads.
+template <int RB, int MAXC, int ACT>
+__device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
+                                           const float* __restrict__ bias, int N, float* out, int ldo) {
+  if ((ldw & 3) == 0 && (K & 3) == 0)
+    tile_dense_impl<RB, MAXC, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo);
+  else
+    tile_dense_impl<RB, MAXC, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo);
+}
+
+// Dispatch on a runtime activation id.
+template <int RB, int MAXC>
+__device__ __forceinline__ void tile_dense_act(int act, const float* in, int ldi, int K, const float* W, int ldw,
+                                               const float* bias, int N, float* out, int ldo) {
+  switch (act) {
+    case ACT_RELU: tile_dense<RB, MAXC, ACT_RELU>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    case ACT_SILU: tile_dense<RB, MAXC, ACT_SILU>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    case ACT_TANH: tile_dense<RB, MAXC, ACT_TANH>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    default: tile_dense<RB, MAXC, ACT_NONE>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+  }
+}
+
+}  // namespace drpo

@@ -1,0 +1,46 @@
+// Library-wide C ABI: version, error reporting.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.hpp"
+
+static thread_local char g_err[1024] = "";
+
+void drpo_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+DRPO_API const char* drpo_last_error(void) { return g_err; }
+
+DRPO_API int drpo_version(void) { return 1; }
+
+// HIP event helpers so hosts without a HIP binding (ctypes/cgo/JNI) can time
+// individual kernels on the stream they run on.
+DRPO_API int drpo_event_create(void** ev) {
+  hipEvent_t e;
+  hipError_t r = hipEventCreate(&e);
+  if (r != hipSuccess) {
+    drpo_set_error("hipEventCreate: %s", hipGetErrorString(r));
+    return DRPO_EHIP;
+  }
+  *ev = (void*)e;
+  return DRPO_OK;
+}
+
+DRPO_API int drpo_event_destroy(void* ev) { return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? DRPO_OK : DRPO_EHIP; }
+
+DRPO_API int drpo_event_record(void* ev, hipStream_t stream) {
+  return hipEventRecord((hipEvent_t)ev, stream) == hipSuccess ? DRPO_OK : DRPO_EHIP;
+}
+
+DRPO_API int drpo_event_elapsed_ms(float* ms, void* start, void* stop) {
+  hipError_t r = hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
+  if (r != hipSuccess) {
+    drpo_set_error("hipEventElapsedTime: %s", hipGetErrorString(r));
+    return DRPO_EHIP;
+  }
+  return DRPO_OK;
+}

@@ -1,0 +1,205 @@
+// Optimizer-side kernels over flat parameter groups (one launch covers a whole
+// group or clip segment, HBM-bound):
+//   drpo_grad_sumsq  : per-block partial sums of g^2 (first pass of clip_grad_norm_)
+//   drpo_adam        : torch.optim.Adam (coupled L2 weight decay, single-tensor
+//                      formulas) with the clip coefficient min(1, max/(||g||+1e-6))
+//                      applied on the fly from the partial sums (deterministic:
+//                      every block reduces the same partials in the same order)
+//   drpo_ema         : target <- rate*p + (1-rate)*target (src/torch_util.py:223-226)
+//   drpo_normalizer_fit : column mean / unbiased std over the replay states
+//                      (src/normalization.py:14-19)
+#include "common.hpp"
+
+using namespace drpo;
+
+static constexpr int SUMSQ_BLOCK_ELEMS = 8192;
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, float* partial) {
+  __shared__ float red[256];
+  const int64_t base = (int64_t)blockIdx.x * SUMSQ_BLOCK_ELEMS;
+  float s = 0.f;
+  for (int64_t i = base + threadIdx.x; i < min(n, base + (int64_t)SUMSQ_BLOCK_ELEMS); i += 256) {
+    const float v = g[i];
+    s = fmaf(v, v, s);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+DRPO_API int drpo_grad_sumsq_blocks(int64_t n) { return (int)((n + SUMSQ_BLOCK_ELEMS - 1) / SUMSQ_BLOCK_ELEMS); }
+
+DRPO_API int drpo_grad_sumsq(const float* g, int64_t n, float* partial, hipStream_t stream) {
+  DRPO_REQUIRE(n >= 0, "drpo_grad_sumsq: n < 0");
+  if (n == 0) return DRPO_OK;
+  sumsq_kernel<<<drpo_grad_sumsq_blocks(n), 256, 0, stream>>>(g, n, partial);
+  DRPO_LAUNCH_CHECK("grad_sumsq");
+  return DRPO_OK;
+}
+
+struct AdamArgs {
+  float* p;
+  const float* g;
+  float *m, *v;
+  int64_t n;
+  float lr_over_bc1;      // lr / (1 - beta1^t)
+  float bc2_sqrt;         // sqrt(1 - beta2^t)
+  float beta1, beta2, one_minus_beta1, one_minus_beta2, eps, wd;
+  const float* partial;   // clip: partial sums of squares (nullptr = no clipping)
+  int n_partial;
+  float max_norm;
+  const float* lr_scale;  // optional device scalar multiplying the step (nullptr = 1)
+};
+
+__device__ __forceinline__ float torch_lerp(float s, float e, float w) {
+  // at::native lerp: w < 0.5 ? s + w*(e-s) : e - (e-s)*(1-w)
+  return (fabsf(w) < 0.5f) ? fmaf(w, e - s, s) : fmaf(-(e - s), 1.f - w, e);
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  __shared__ float s_coef;
+  if (a.partial) {
+    if (threadIdx.x < 64) {
+      float s = 0.f;
+      for (int i = threadIdx.x; i < a.n_partial; i += 64) s += a.partial[i];
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+      if (threadIdx.x == 0) {
+        const float norm = sqrtf(s);
+        const float c = a.max_norm / (norm + 1e-6f);
+        s_coef = c < 1.f ? c : 1.f;
+      }
+    }
+    __syncthreads();
+  }
+  const float coef = a.partial ? s_coef : 1.f;
+  const float step = a.lr_over_bc1 * (a.lr_scale ? *a.lr_scale : 1.f);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float p = a.p[i];
+    float g = a.g[i] * coef;
+    if (a.wd != 0.f) g = fmaf(p, a.wd, g);
+    const float m = torch_lerp(a.m[i], g, a.one_minus_beta1);
+    const float v = fmaf(a.v[i], a.beta2, a.one_minus_beta2 * g * g);
+    a.m[i] = m;
+    a.v[i] = v;
+    const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+    a.p[i] = p - step * (m / denom);
+  }
+}
+
+DRPO_API int drpo_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_over_bc1, float bc2_sqrt,
+                       float beta1, float beta2, float eps, float weight_decay, const float* clip_partial,
+                       int n_partial, float max_norm, const float* lr_scale, hipStream_t stream) {
+  DRPO_REQUIRE(n >= 0 && p && g && m && v, "drpo_adam: bad arguments");
+  if (n == 0) return DRPO_OK;
+  AdamArgs a{p, g, m, v, n, lr_over_bc1, bc2_sqrt, beta1, beta2, 1.f - beta1, 1.f - beta2, eps, weight_decay,
+             clip_partial, n_partial, max_norm, lr_scale};
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  adam_kernel<<<blocks, 256, 0, stream>>>(a);
+  DRPO_LAUNCH_CHECK("adam");
+  return DRPO_OK;
+}
+
+__global__ void ema_kernel(float* t, const float* p, int64_t n, float rate, float keep) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    t[i] = rate * p[i] + keep * t[i];
+}
+
+DRPO_API int drpo_ema(float* target, const float* source, int64_t n, float rate, hipStream_t stream) {
+  DRPO_REQUIRE(rate >= 0.f && rate <= 1.f, "drpo_ema: rate must be in [0,1]");
+  if (n == 0) return DRPO_OK;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  // (1 - rate) is formed in double like the Python reference, then rounded once
+  ema_kernel<<<blocks, 256, 0, stream>>>(target, source, n, rate, (float)(1.0 - (double)rate));
+  DRPO_LAUNCH_CHECK("ema");
+  return DRPO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Normalizer.fit: column mean and unbiased std over X [N][S] (double accumulation)
+// ---------------------------------------------------------------------------
+static constexpr int NORM_ROWS = 2048;
+
+__global__ __launch_bounds__(256) void colstats_partial_kernel(const float* X, int64_t N, int S, double* part) {
+  // block b: rows [b*NORM_ROWS, ...); thread t: column t % S, row lane t / S
+  extern __shared__ double sh[];
+  const int lanes = 256 / S;
+  const int c = threadIdx.x % S, rl = threadIdx.x / S;
+  double s = 0.0, q = 0.0;
+  if (rl < lanes) {
+    const int64_t r0 = (int64_t)blockIdx.x * NORM_ROWS;
+    const int64_t r1 = min(N, r0 + NORM_ROWS);
+    for (int64_t r = r0 + rl; r < r1; r += lanes) {
+      const double x = X[r * S + c];
+      s += x;
+      q += x * x;
+    }
+  }
+  sh[threadIdx.x] = (rl < lanes) ? s : 0.0;
+  sh[256 + threadIdx.x] = (rl < lanes) ? q : 0.0;
+  __syncthreads();
+  if (threadIdx.x < S) {
+    double ts = 0.0, tq = 0.0;
+    for (int l = 0; l < lanes; ++l) {
+      ts += sh[l * S + threadIdx.x];
+      tq += sh[256 + l * S + threadIdx.x];
+    }
+    part[(int64_t)blockIdx.x * 2 * S + threadIdx.x] = ts;
+    part[(int64_t)blockIdx.x * 2 * S + S + threadIdx.x] = tq;
+  }
+}
+
+__global__ void colstats_final_kernel(const double* part, int nb, int64_t N, int S, float* mean, float* std) {
+  const int c = threadIdx.x;
+  if (c >= S) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    s += part[(int64_t)b * 2 * S + c];
+    q += part[(int64_t)b * 2 * S + S + c];
+  }
+  const double mu = s / (double)N;
+  double var = N > 1 ? (q - s * mu) / (double)(N - 1) : __longlong_as_double(0x7ff8000000000000LL);
+  if (var < 0) var = 0;
+  float sd = (float)sqrt(var);
+  if (!(sd >= 1e-6f)) sd = (sd < 1e-6f) ? 1.0f : sd;   // std[std < 1e-6] = 1.0 (NaN stays NaN)
+  mean[c] = (float)mu;
+  std[c] = sd;
+}
+
+DRPO_API size_t drpo_normalizer_workspace_size(int64_t N, int S) {
+  return sizeof(double) * 2 * (size_t)S * (size_t)((N + NORM_ROWS - 1) / NORM_ROWS);
+}
+
+DRPO_API int drpo_normalizer_fit(const float* X, int64_t N, int S, float* mean, float* std, void* workspace,
+                                 hipStream_t stream) {
+  DRPO_REQUIRE(N >= 1 && S >= 1 && S <= 256, "drpo_normalizer_fit: N=%lld S=%d", (long long)N, S);
+  const int nb = (int)((N + NORM_ROWS - 1) / NORM_ROWS);
+  colstats_partial_kernel<<<nb, 256, 2 * 256 * sizeof(double), stream>>>(X, N, S, (double*)workspace);
+  DRPO_LAUNCH_CHECK("normalizer_partial");
+  colstats_final_kernel<<<1, 256, 0, stream>>>((const double*)workspace, nb, N, S, mean, std);
+  DRPO_LAUNCH_CHECK("normalizer_final");
+  return DRPO_OK;
+}
+
+__global__ void normalize_kernel(const float* x, const float* mean, const float* std, float eps, float* y,
+                                 int64_t n, int S) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * S; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % S);
+    y[i] = (x[i] - mean[c]) / (std[c] + eps);
+  }
+}
+
+DRPO_API int drpo_normalize(const float* x, const float* mean, const float* std, float eps, float* y, int64_t n,
+                            int S, hipStream_t stream) {
+  if (n == 0) return DRPO_OK;
+  int64_t blocks = (n * S + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  normalize_kernel<<<(unsigned)blocks, 256, 0, stream>>>(x, mean, std, eps, y, n, S);
+  DRPO_LAUNCH_CHECK("normalize");
+  return DRPO_OK;
+}

@@ -1,0 +1,524 @@
+// Fused imagined-rollout step (SMBPO.rollout, src/smbpo.py:229-249).
+//
+// One launch of rollout_step_kernel processes one horizon step for every alive
+// row: each 256-thread workgroup owns a 16- or 32-row tile and keeps all of its
+// activations in LDS while it runs
+//   actor MLP S->H->H->2A (ReLU)  +  squashed-Gaussian sample   (src/policy.py:89-97)
+//   elite member MLP trunk/diff/log-var heads (SiLU) + log-var clamp + Gaussian
+//   sample                                                      (src/dynamics.py:112-122,198-203)
+//   env constraint functions                                    (env_constraints.hpp)
+//   the 7-component row write into the circular virtual buffer  (src/sampling.py:128-145)
+// and emits per-tile alive counts plus an in-tile compaction map. The next step's
+// launch performs the order-preserving `next_states[~dones]` compaction
+// (src/smbpo.py:243-246) itself: each workgroup scans the previous step's tile
+// counts and binary-searches the source row of each of its rows, so a horizon
+// step is ONE launch. Row counts and buffer offsets live on the device, so a whole
+// rollout needs no host synchronisation.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.hpp"
+#include "env_constraints.hpp"
+
+using namespace drpo;
+
+struct RolloutStepArgs {
+  int S, A, C, Ha, Hm, t, Bmax;
+  EnvParams env;
+  // actor (row-major [out][in] weights)
+  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;
+  // elite member slices of the ensemble
+  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2;
+  const float *norm_mean, *norm_std, *min_lv, *max_lv;
+  // step-0 source: replay buffer states (physical layout) + chronological indices
+  const float* replay_states;
+  const int64_t* init_idx;        // nullptr -> device PRP sample without replacement
+  int64_t replay_len, replay_ptr, replay_cap;
+  uint32_t prp_key[4];
+  int prp_half_bits;
+  // step t>0 source: previous step's next states + compaction map
+  const float* prev_nxt;
+  const int* prev_cnt;
+  const int* prev_inv;
+  // device step bookkeeping (n[t], off[t] written by workgroup 0 of step t)
+  int* n;
+  int64_t* off;
+  // noise: parity mode (caller-provided eps rows for this step) or Philox
+  const float* eps_a;             // [Bmax][A]
+  const float* eps_m;             // [Bmax][S+1]
+  uint64_t seed, ctr;
+  // virtual buffer
+  float *vs, *va, *vs2, *vr, *vh;
+  uint8_t *vd, *vv;
+  const int64_t* vptr;
+  int64_t vcap;
+  // this step's outputs for the next step
+  float* nxt;
+  int* cnt;
+  int* inv;
+  // LDS strides
+  int ldx, ldh, ldm, lds;
+};
+
+__device__ __forceinline__ uint32_t prp_round(uint32_t r, uint32_t k) {
+  uint32_t h = r * 0x9E3779B1u ^ k;
+  h ^= h >> 15;
+  h *= 0x85EBCA77u;
+  h ^= h >> 13;
+  h *= 0xC2B2AE3Du;
+  h ^= h >> 16;
+  return h;
+}
+
+// Keyed 4-round Feistel permutation of [0, 2^(2*hb)) with cycle walking into
+// [0, N): the first B outputs are B distinct indices (sampling without
+// replacement, the production stand-in for np.random.choice(N, B, replace=False)).
+__device__ inline int64_t prp_index(uint64_t i, uint64_t N, int hb, const uint32_t key[4]) {
+  const uint32_t mask = (hb >= 32) ? 0xFFFFFFFFu : ((1u << hb) - 1u);
+  uint64_t x = i;
+  for (int it = 0; it < 64; ++it) {
+    uint32_t L = (uint32_t)(x >> hb) & mask, R = (uint32_t)x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      uint32_t F = prp_round(R, key[r]) & mask;
+      uint32_t nl = R;
+      R = L ^ F;
+      L = nl;
+    }
+    x = ((uint64_t)L << hb) | R;
+    if (x < N) return (int64_t)x;
+  }
+  return (int64_t)(x % N);   // unreachable in practice (expected walk < 4)
+}
+
+template <int RB>
+__global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
+  constexpr int ROWS = RB * 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int S = p.S, A = p.A, C = p.C, S1 = p.S + 1;
+
+  float* xin = smem;                       // ROWS x ldx  actor in / model in / next states
+  float* h1 = xin + ROWS * p.ldx;          // ROWS x ldh
+  float* h2 = h1 + ROWS * p.ldh;           // ROWS x ldh
+  float* sraw = h2 + ROWS * p.ldh;         // ROWS x lds  raw states
+  float* ao = sraw + ROWS * p.lds;         // ROWS x 20   actor head
+  float* dout = ao + ROWS * 20;            // ROWS x ldm  diff head
+  float* lout = dout + ROWS * p.ldm;       // ROWS x ldm  log-var head
+  float* act = lout + ROWS * p.ldm;        // ROWS x 8    sampled actions
+  float* rew = act + ROWS * 8;             // ROWS
+  float* hval = rew + ROWS;                // ROWS x 8    constraint values
+  int* flags = reinterpret_cast<int*>(hval + ROWS * 8);   // ROWS: bit0 done, bit1 violation
+  int* srcrow = flags + ROWS;                              // ROWS
+  int* s_part = srcrow + ROWS;                             // 256 scan partials
+  int* scan = s_part + 256;                                // prev tiles + 1 (exclusive prefix)
+
+  // ---- 0. row count / buffer offset of this step + compaction map ----------
+  int n;
+  int64_t off;
+  const int row0 = blockIdx.x * ROWS;
+  if (p.t == 0) {
+    n = p.Bmax;
+    off = 0;
+  } else {
+    const int n_prev = p.n[p.t - 1];
+    const int T = (n_prev + ROWS - 1) / ROWS;
+    // exclusive scan of the previous step's tile counts (T <= ntiles), 256 threads
+    const int per = (T + 255) / 256;
+    const int b0 = tid * per;
+    int run = 0;
+    for (int i = 0; i < per; ++i) {
+      const int ti = b0 + i;
+      if (ti < T) {
+        scan[ti] = run;
+        run += p.prev_cnt[ti];
+      }
+    }
+    s_part[tid] = run;
+    __syncthreads();
+    if (tid < 64) {   // exclusive scan of the 256 partials in one wave
+      int v[4], sum = 0;
+      for (int q = 0; q < 4; ++q) { v[q] = s_part[tid * 4 + q]; sum += v[q]; }
+      int incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += y;
+      }
+      int e = incl - sum;
+      for (int q = 0; q < 4; ++q) { const int x = v[q]; s_part[tid * 4 + q] = e; e += x; }
+    }
+    __syncthreads();
+    for (int i = 0; i < per; ++i) {
+      const int ti = b0 + i;
+      if (ti < T) scan[ti] += s_part[tid];
+    }
+    if (tid == 255) scan[T] = s_part[255] + run;    // total alive == n for this step
+    __syncthreads();
+    n = scan[T];
+    off = p.off[p.t - 1] + n_prev;
+    if (tid < ROWS && row0 + tid < n) {   // binary search: last tile with scan[tile] <= i
+      const int i = row0 + tid;
+      int lo = 0, hi = T - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (scan[mid] <= i) lo = mid; else hi = mid - 1;
+      }
+      srcrow[tid] = lo * ROWS + p.prev_inv[lo * ROWS + (i - scan[lo])];
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    p.n[p.t] = n;
+    p.off[p.t] = off;
+  }
+  if (row0 >= n) return;
+  const int rows = min(ROWS, n - row0);
+  const int64_t vbase = *p.vptr + off + row0;
+  __syncthreads();
+
+  // ---- 1. gather the tile's states (zero-padded) ---------------------------
+  const int kpad = round_up(S + A, 16);
+  for (int e = tid; e < ROWS * kpad; e += WG) {
+    const int r = e / kpad, k = e - r * kpad;
+    float v = 0.f;
+    if (r < rows && k < S) {
+      if (p.t == 0) {
+        int64_t c = p.init_idx ? p.init_idx[row0 + r]
+                               : prp_index((uint64_t)(row0 + r), (uint64_t)p.replay_len, p.prp_half_bits, p.prp_key);
+        int64_t phys = (p.replay_ptr > p.replay_cap) ? (p.replay_ptr % p.replay_cap + c) % p.replay_cap : c;
+        v = p.replay_states[phys * S + k];
+      } else {
+        v = p.prev_nxt[(int64_t)srcrow[r] * S + k];
+      }
+    }
+    xin[r * p.ldx + k] = v;
+    if (k < S) sraw[r * p.lds + k] = v;
+  }
+  __syncthreads();
+
+  // ---- 2. actor MLP (src/policy.py:61-100; mlp() ReLU hidden) ---------------
+  tile_dense<RB, 4, ACT_RELU>(xin, p.ldx, S, p.aW1, S, p.ab1, p.Ha, h1, p.ldh);
+  __syncthreads();
+  tile_dense<RB, 4, ACT_RELU>(h1, p.ldh, p.Ha, p.aW2, p.Ha, p.ab2, p.Ha, h2, p.ldh);
+  __syncthreads();
+  tile_dense<RB, 1, ACT_NONE>(h2, p.ldh, p.Ha, p.aW3, p.Ha, p.ab3, 2 * A, ao, 20);
+  __syncthreads();
+
+  // ---- 3. squashed Gaussian sample + model input [normalize(s), a] ----------
+  for (int e = tid; e < ROWS * A; e += WG) {
+    const int r = e / A, d = e - r * A;
+    const float mu = ao[r * 20 + d], raw = ao[r * 20 + A + d];
+    const float ls = -6.f + 10.f * sigmoidf(raw);
+    const float sd = expf(ls) * 1.0f;
+    float eps;
+    if (p.eps_a) {
+      eps = (r < rows) ? p.eps_a[(int64_t)(row0 + r) * A + d] : 0.f;
+    } else {
+      float z[4];
+      philox_normal4(p.seed, (uint32_t)(row0 + r), ((uint32_t)p.t << 8) | 0u, (uint32_t)(d >> 2), (uint32_t)p.ctr, z);
+      eps = z[d & 3];
+    }
+    const float a = tanhf(eps * sd + mu);
+    act[r * 8 + d] = a;
+    xin[r * p.ldx + S + d] = a;
+  }
+  for (int e = tid; e < ROWS * S; e += WG) {
+    const int r = e / S, k = e - r * S;
+    xin[r * p.ldx + k] = (sraw[r * p.lds + k] - p.norm_mean[k]) / (p.norm_std[k] + 1e-6f);
+  }
+  __syncthreads();
+
+  // ---- 4. elite member forward (src/dynamics.py:112-122, swish) -------------
+  tile_dense<RB, 4, ACT_SILU>(xin, p.ldx, S + A, p.mW1, S + A, p.mb1, p.Hm, h1, p.ldh);
+  __syncthreads();
+  tile_dense<RB, 4, ACT_SILU>(h1, p.ldh, p.Hm, p.mW2, p.Hm, p.mb2, p.Hm, h2, p.ldh);
+  __syncthreads();
+  tile_dense<RB, 4, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.Hm, p.db1, p.Hm, h1, p.ldh);
+  __syncthreads();
+  tile_dense<RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.Hm, p.db2, S1, dout, p.ldm);
+  __syncthreads();
+  tile_dense<RB, 4, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.Hm, p.lb1, p.Hm, h1, p.ldh);
+  __syncthreads();
+  tile_dense<RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.Hm, p.lb2, S1, lout, p.ldm);
+  __syncthreads();
+
+  // ---- 5. residual mean, log-var soft clamp, Gaussian sample ---------------
+  for (int e = tid; e < ROWS * S1; e += WG) {
+    const int r = e / S1, j = e - r * S1;
+    const float mean = dout[r * p.ldm + j] + (j < S ? sraw[r * p.lds + j] : 0.f);
+    float lv = lout[r * p.ldm + j];
+    lv = p.max_lv[j] - softplusf(p.max_lv[j] - lv);
+    lv = p.min_lv[j] + softplusf(lv - p.min_lv[j]);
+    const float sd = sqrtf(expf(lv));
+    float eps;
+    if (p.eps_m) {
+      eps = (r < rows) ? p.eps_m[(int64_t)(row0 + r) * S1 + j] : 0.f;
+    } else {
+      float z[4];
+      philox_normal4(p.seed, (uint32_t)(row0 + r), ((uint32_t)p.t << 8) | 1u, (uint32_t)(j >> 2), (uint32_t)p.ctr, z);
+      eps = z[j & 3];
+    }
+    const float x = mean + sd * eps;
+    if (j < S) xin[r * p.ldx + j] = x;
+    else rew[r] = x;
+  }
+  __syncthreads();
+
+  // ---- 6. constraints + in-tile compaction ranks ---------------------------
+  if (tid < 64) {
+    bool alive_r = false;
+    if (tid < rows) {
+      bool dn, vl;
+      float hh[8];
+      env_constraints_row(p.env, xin + tid * p.ldx, dn, vl, hh);
+      for (int c = 0; c < C; ++c) hval[tid * 8 + c] = hh[c];
+      flags[tid] = (dn ? 1 : 0) | (vl ? 2 : 0);
+      alive_r = !dn;
+    }
+    const uint64_t m = __ballot(alive_r);
+    if (alive_r) p.inv[row0 + __popcll(m & ((1ull << tid) - 1ull))] = tid;   // k-th alive row of the tile
+    if (tid == 0) p.cnt[blockIdx.x] = __popcll(m);
+  }
+  __syncthreads();
+
+  // ---- 7. row writes into the circular virtual buffer + next-state scratch --
+  for (int e = tid; e < rows * S; e += WG) {
+    const int r = e / S, k = e - r * S;
+    const int64_t q = (vbase + r) % p.vcap;
+    p.vs[q * S + k] = sraw[r * p.lds + k];
+    const float x = xin[r * p.ldx + k];
+    p.vs2[q * S + k] = x;
+    p.nxt[(int64_t)(row0 + r) * S + k] = x;
+  }
+  for (int e = tid; e < rows * A; e += WG) {
+    const int r = e / A, d = e - r * A;
+    p.va[((vbase + r) % p.vcap) * A + d] = act[r * 8 + d];
+  }
+  for (int e = tid; e < rows * C; e += WG) {
+    const int r = e / C, c = e - r * C;
+    p.vh[((vbase + r) % p.vcap) * C + c] = hval[r * 8 + c];
+  }
+  if (tid < rows) {
+    const int64_t q = (vbase + tid) % p.vcap;
+    p.vr[q] = rew[tid];
+    p.vd[q] = flags[tid] & 1;
+    p.vv[q] = (flags[tid] >> 1) & 1;
+  }
+}
+
+// total rows written = off[H-1] + n[H-1]; advance the buffer pointer
+__global__ void rollout_finalize_kernel(int64_t* vptr, const int* n, int64_t* off, int H) {
+  const int64_t total = off[H - 1] + n[H - 1];
+  off[H] = total;
+  *vptr += total;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+typedef struct {
+  int S, A, C, Ha, Hm, B, H;
+  int env_id, tracking_surr_start, tracking_n_surr;
+  float quad_x_threshold, quad_z_threshold;
+  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;
+  // ensemble parameters [E][out][in] / [E][out]
+  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2;
+  const float *norm_mean, *norm_std, *min_lv, *max_lv;
+  const int* members;              // host array [H]: elite member used at each step
+  const float* replay_states;
+  int64_t replay_ptr, replay_cap;
+  const int64_t* init_idx;         // device [B] chronological indices, or NULL (device PRP)
+  const float* eps_a;              // device [H][B][A] or NULL (Philox)
+  const float* eps_m;              // device [H][B][S+1] or NULL
+  uint64_t seed, ctr;
+  float *vs, *va, *vs2, *vr, *vh;
+  uint8_t *vd, *vv;
+  int64_t* vptr;                   // device: buffer pointer (advanced by the rollout)
+  int64_t vcap;
+  void* workspace;
+  int rows_per_tile;               // 16 or 32 (0: auto)
+  void** step_events;              // optional [2*H] hipEvent_t recorded around each step kernel
+} drpo_rollout_desc_t;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct RolloutWs {
+  float* nxt[2];
+  int* cnt[2];
+  int* inv[2];
+  int* n;
+  int64_t* off;
+};
+
+// Byte offsets of the workspace pieces (in order); returns total bytes.
+static size_t rollout_ws_offsets(int B, int S, int H, size_t off[8]) {
+  const size_t bytes[8] = {sizeof(float) * (size_t)B * S, sizeof(float) * (size_t)B * S,
+                           sizeof(int) * ((size_t)B / 16 + 1), sizeof(int) * ((size_t)B / 16 + 1),
+                           sizeof(int) * (size_t)B, sizeof(int) * (size_t)B,
+                           sizeof(int) * (size_t)(H + 1), sizeof(int64_t) * (size_t)(H + 1)};
+  size_t o = 0;
+  for (int i = 0; i < 8; ++i) {
+    off[i] = o;
+    o += align256(bytes[i]);
+  }
+  return o;
+}
+
+static RolloutWs rollout_ws(int B, int S, int H, char* base) {
+  size_t o[8];
+  rollout_ws_offsets(B, S, H, o);
+  RolloutWs w;
+  w.nxt[0] = (float*)(base + o[0]);
+  w.nxt[1] = (float*)(base + o[1]);
+  w.cnt[0] = (int*)(base + o[2]);
+  w.cnt[1] = (int*)(base + o[3]);
+  w.inv[0] = (int*)(base + o[4]);
+  w.inv[1] = (int*)(base + o[5]);
+  w.n = (int*)(base + o[6]);
+  w.off = (int64_t*)(base + o[7]);
+  return w;
+}
+
+DRPO_API size_t drpo_rollout_workspace_size(int B, int S, int H) {
+  size_t o[8];
+  return rollout_ws_offsets(B, S, H, o);
+}
+
+// Byte offset (inside the workspace) of the device int64 that holds the number of
+// transitions written by the last drpo_rollout call (off[H]).
+DRPO_API size_t drpo_rollout_count_offset(int B, int S, int H) {
+  size_t o[8];
+  rollout_ws_offsets(B, S, H, o);
+  return o[7] + sizeof(int64_t) * (size_t)H;
+}
+
+static int hb_for(int64_t n) {
+  int b = 1;
+  while ((1ull << (2 * b)) < (uint64_t)n) ++b;
+  return b;
+}
+
+DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, hipStream_t stream) {
+  DRPO_REQUIRE(d, "drpo_rollout: null descriptor");
+  DRPO_REQUIRE(d->S >= 1 && d->S <= 64 && d->A >= 1 && d->A <= 8, "drpo_rollout: S=%d A=%d out of range", d->S, d->A);
+  DRPO_REQUIRE(d->Ha >= 1 && d->Ha <= 256 && d->Hm >= 1 && d->Hm <= 256, "drpo_rollout: hidden dims must be <= 256");
+  DRPO_REQUIRE(d->S + 1 <= 64, "drpo_rollout: state_dim+1 must be <= 64");
+  DRPO_REQUIRE(d->C >= 1 && d->C <= 8 && d->C == env_con_dim(d->env_id, d->tracking_n_surr),
+               "drpo_rollout: con_dim %d does not match env %d", d->C, d->env_id);
+  DRPO_REQUIRE(d->B >= 1 && d->H >= 1 && (int64_t)d->B * d->H <= d->vcap,
+               "drpo_rollout: B*H=%lld exceeds buffer capacity %lld", (long long)d->B * d->H, (long long)d->vcap);
+  DRPO_REQUIRE(d->workspace && d->vptr && d->replay_states, "drpo_rollout: null pointer");
+  DRPO_REQUIRE(d->B <= 16 * 8192, "drpo_rollout: batch %d too large (max 131072)", d->B);
+  const int64_t rlen = d->replay_ptr < d->replay_cap ? d->replay_ptr : d->replay_cap;
+  DRPO_REQUIRE(rlen >= d->B, "drpo_rollout: replay has %lld rows < batch %d (sampling without replacement)",
+               (long long)rlen, d->B);
+  if (d->env_id == ENV_TRACKING)
+    DRPO_REQUIRE(d->tracking_surr_start + 4 * d->tracking_n_surr <= d->S, "drpo_rollout: tracking layout");
+
+  RolloutWs w = rollout_ws(d->B, d->S, d->H, (char*)d->workspace);
+  const int rpt = d->rows_per_tile ? d->rows_per_tile : (d->B >= 256 * 32 ? 32 : 16);
+  DRPO_REQUIRE(rpt == 16 || rpt == 32, "drpo_rollout: rows_per_tile must be 16 or 32");
+  const int S = d->S, A = d->A, S1 = d->S + 1;
+
+  RolloutStepArgs a{};
+  a.S = S; a.A = A; a.C = d->C; a.Ha = d->Ha; a.Hm = d->Hm; a.Bmax = d->B;
+  a.env.id = d->env_id; a.env.surr_start = d->tracking_surr_start; a.env.n_surr = d->tracking_n_surr;
+  a.env.quad_x_threshold = d->quad_x_threshold; a.env.quad_z_threshold = d->quad_z_threshold;
+  a.aW1 = d->aW1; a.ab1 = d->ab1; a.aW2 = d->aW2; a.ab2 = d->ab2; a.aW3 = d->aW3; a.ab3 = d->ab3;
+  a.norm_mean = d->norm_mean; a.norm_std = d->norm_std; a.min_lv = d->min_lv; a.max_lv = d->max_lv;
+  a.replay_states = d->replay_states; a.init_idx = d->init_idx;
+  a.replay_len = rlen; a.replay_ptr = d->replay_ptr; a.replay_cap = d->replay_cap;
+  a.prp_half_bits = hb_for(rlen);
+  for (int i = 0; i < 4; ++i) a.prp_key[i] = (uint32_t)(d->seed >> (8 * i)) * 0x9E3779B9u + (uint32_t)d->ctr * (2 * i + 1) + i;
+  a.seed = d->seed; a.ctr = d->ctr;
+  a.vs = d->vs; a.va = d->va; a.vs2 = d->vs2; a.vr = d->vr; a.vh = d->vh; a.vd = d->vd; a.vv = d->vv;
+  a.vptr = d->vptr; a.vcap = d->vcap;
+  a.n = w.n; a.off = w.off;
+  a.ldx = lds_ld(S + A);
+  a.ldh = lds_ld(d->Ha > d->Hm ? d->Ha : d->Hm);
+  a.ldm = round_up(S1, 16) + 4;
+  a.lds = round_up(S, 4);
+
+  const int tiles = (d->B + rpt - 1) / rpt;
+  const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 2 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 2) +
+                                            (size_t)tiles + 1 + 256);
+  DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
+
+  const int E_out_in[6][2] = {{d->Hm, S + A}, {d->Hm, d->Hm}, {d->Hm, d->Hm}, {S1, d->Hm}, {d->Hm, d->Hm}, {S1, d->Hm}};
+  const float* Wb[6] = {d->mW1, d->mW2, d->dW1, d->dW2, d->lW1, d->lW2};
+  const float* Bb[6] = {d->mb1, d->mb2, d->db1, d->db2, d->lb1, d->lb2};
+
+  for (int t = 0; t < d->H; ++t) {
+    const int m = d->members[t];
+    const float* Wm[6];
+    const float* Bm[6];
+    for (int i = 0; i < 6; ++i) {
+      Wm[i] = Wb[i] + (size_t)m * E_out_in[i][0] * E_out_in[i][1];
+      Bm[i] = Bb[i] + (size_t)m * E_out_in[i][0];
+    }
+    a.mW1 = Wm[0]; a.mW2 = Wm[1]; a.dW1 = Wm[2]; a.dW2 = Wm[3]; a.lW1 = Wm[4]; a.lW2 = Wm[5];
+    a.mb1 = Bm[0]; a.mb2 = Bm[1]; a.db1 = Bm[2]; a.db2 = Bm[3]; a.lb1 = Bm[4]; a.lb2 = Bm[5];
+    a.t = t;
+    const int cur = t & 1, prv = cur ^ 1;
+    a.prev_nxt = w.nxt[prv]; a.prev_cnt = w.cnt[prv]; a.prev_inv = w.inv[prv];
+    a.nxt = w.nxt[cur]; a.cnt = w.cnt[cur]; a.inv = w.inv[cur];
+    a.eps_a = d->eps_a ? d->eps_a + (size_t)t * d->B * A : nullptr;
+    a.eps_m = d->eps_m ? d->eps_m + (size_t)t * d->B * S1 : nullptr;
+    if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[2 * t], stream);
+    if (rpt == 32)
+      rollout_step_kernel<2><<<tiles, 256, lds_bytes, stream>>>(a);
+    else
+      rollout_step_kernel<1><<<tiles, 256, lds_bytes, stream>>>(a);
+    DRPO_LAUNCH_CHECK("rollout_step");
+    if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[2 * t + 1], stream);
+  }
+  rollout_finalize_kernel<<<1, 1, 0, stream>>>(d->vptr, w.n, w.off, d->H);
+  DRPO_LAUNCH_CHECK("rollout_finalize");
+  return DRPO_OK;
+}
+
+// Standalone batched constraint evaluation (tests, evaluation, robust target).
+__global__ void env_constraints_kernel(EnvParams ep, const float* s, int64_t n, int S, int C, uint8_t* done,
+                                       uint8_t* viol, float* h) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool dn, vl;
+  float hh[8];
+  env_constraints_row(ep, s + i * S, dn, vl, hh);
+  if (done) done[i] = dn;
+  if (viol) viol[i] = vl;
+  if (h)
+    for (int c = 0; c < C; ++c) h[i * C + c] = hh[c];
+}
+
+DRPO_API int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, float quad_x_threshold,
+                                  float quad_z_threshold, const float* states, int64_t n, int S, uint8_t* done,
+                                  uint8_t* violation, float* h, hipStream_t stream) {
+  DRPO_REQUIRE(env_id >= 0 && env_id <= 3, "drpo_env_constraints: unknown env id %d", env_id);
+  if (n == 0) return DRPO_OK;
+  EnvParams ep{env_id, tracking_surr_start, tracking_n_surr, quad_x_threshold, quad_z_threshold};
+  const int C = env_con_dim(env_id, tracking_n_surr);
+  env_constraints_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ep, states, n, S, C, done, violation, h);
+  DRPO_LAUNCH_CHECK("env_constraints");
+  return DRPO_OK;
+}
+
+__global__ void prp_kernel(int64_t* out, int64_t B, int64_t N, int hb, uint32_t k0, uint32_t k1, uint32_t k2,
+                           uint32_t k3) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const uint32_t key[4] = {k0, k1, k2, k3};
+  out[i] = prp_index((uint64_t)i, (uint64_t)N, hb, key);
+}
+
+DRPO_API int drpo_sample_without_replacement(int64_t* out, int64_t B, int64_t N, uint64_t seed, uint64_t ctr,
+                                             hipStream_t stream) {
+  DRPO_REQUIRE(B >= 0 && B <= N && N < (1ll << 62), "drpo_sample_without_replacement: need 0 <= B <= N");
+  if (B == 0) return DRPO_OK;
+  uint32_t k[4];
+  for (int i = 0; i < 4; ++i) k[i] = (uint32_t)(seed >> (8 * i)) * 0x9E3779B9u + (uint32_t)ctr * (2 * i + 1) + i;
+  prp_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(out, B, N, hb_for(N), k[0], k[1], k[2], k[3]);
+  DRPO_LAUNCH_CHECK("prp");
+  return DRPO_OK;
+}

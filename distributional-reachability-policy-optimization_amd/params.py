@@ -1,0 +1,144 @@
+"""Flat, HBM-resident parameter groups with reference-compatible module trees.
+
+Every optimizer group of the reference (critic+constraint critic, actor, safe actor,
+multiplier, model ensemble) lives in ONE contiguous fp32 buffer, with matching
+flat buffers for gradients and Adam moments. The ``nn.Parameter`` objects the
+user sees (and that ``state_dict`` / ``load_state_dict`` touch) are views into
+that buffer, laid out exactly like the reference's ``mlp()`` Sequentials
+(src/torch_util.py:190-211) so checkpoints keep their key names and shapes.
+One flat buffer per group means one kernel for Adam / grad-norm / EMA and one
+RCCL bucket per group for data parallelism.
+
+Initialisation replays the reference's CPU-RNG consumption order exactly
+(nn.Linear construction + xavier_normal_ / zeros_ from weight_initializer,
+src/torch_util.py:146-155; BatchedLinear's (E+1) nn.Linear resets,
+src/dynamics.py:26-47), so for a given torch seed the initial weights are
+bit-identical to the reference's.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64   # floats: every tensor starts 256-byte aligned (float4 weight loads)
+
+
+class FlatGroup:
+    """Contiguous storage for one parameter group (+ grad / Adam m / v)."""
+
+    def __init__(self, name):
+        self.name = name
+        self.entries = {}      # name -> (offset, shape)
+        self.order = []
+        self.size = 0
+        self.data = None
+        self.grad = None
+
+    def add(self, name, shape):
+        n = int(math.prod(shape))
+        self.entries[name] = (self.size, tuple(shape))
+        self.order.append(name)
+        self.size += (n + ALIGN - 1) // ALIGN * ALIGN
+        return name
+
+    def allocate(self, device):
+        self.data = torch.zeros(self.size, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.size, dtype=torch.float32, device=device)
+        return self
+
+    def view(self, name, buf=None):
+        off, shape = self.entries[name]
+        n = int(math.prod(shape))
+        b = self.data if buf is None else buf
+        return b[off:off + n].view(shape)
+
+    def offset(self, name):
+        return self.entries[name][0]
+
+    def span(self, prefix):
+        """(start, end) floats covering all entries whose name starts with prefix."""
+        offs = [(self.entries[n][0], self.entries[n][0] + int(math.prod(self.entries[n][1])))
+                for n in self.order if n.startswith(prefix)]
+        return min(o[0] for o in offs), max(o[1] for o in offs)
+
+
+class LinearSlot(nn.Module):
+    """Parameter-holding stand-in for nn.Linear / BatchedLinear (weight [.., out, in], bias [.., out])."""
+
+    def __init__(self, group, prefix):
+        super().__init__()
+        self.weight = nn.Parameter(group.view(prefix + 'weight'), requires_grad=False)
+        self.bias = nn.Parameter(group.view(prefix + 'bias'), requires_grad=False)
+        if group.grad is not None:          # target groups (frozen) carry no gradient storage
+            self.weight.grad = group.view(prefix + 'weight', group.grad)
+            self.bias.grad = group.view(prefix + 'bias', group.grad)
+
+
+class Squeeze(nn.Module):
+    def forward(self, x):
+        return x.squeeze(1)
+
+
+_ACT = {'relu': nn.ReLU, 'tanh': nn.Tanh, 'swish': nn.SiLU, 'identity': nn.Identity}
+
+
+class MLPSpec:
+    """Shape of one mlp(): dims, hidden activation, output activation, squeeze."""
+
+    def __init__(self, dims, act='relu', out_act=None, squeeze=False, ensemble=None):
+        self.dims, self.act, self.out_act, self.squeeze, self.E = list(dims), act, out_act, squeeze, ensemble
+
+    @property
+    def n_layers(self):
+        return len(self.dims) - 1
+
+    def layer_shapes(self):
+        for i in range(self.n_layers):
+            din, dout = self.dims[i], self.dims[i + 1]
+            if self.E is None:
+                yield 2 * i, (dout, din), (dout,)
+            else:
+                yield 2 * i, (self.E, dout, din), (self.E, dout)
+
+    def register(self, group, prefix):
+        for idx, ws, bs in self.layer_shapes():
+            group.add(f'{prefix}{idx}.weight', ws)
+            group.add(f'{prefix}{idx}.bias', bs)
+
+    def build(self, group, prefix):
+        """nn.Sequential with Linear slots at the reference's indices."""
+        layers = []
+        for i in range(self.n_layers):
+            layers.append(LinearSlot(group, f'{prefix}{2 * i}.'))
+            if i < self.n_layers - 1:
+                layers.append(_ACT[self.act]())
+        if self.out_act is not None:
+            layers.append(_ACT[self.out_act]())
+        if self.squeeze and self.dims[-1] == 1:
+            layers.append(Squeeze())
+        return nn.Sequential(*layers)
+
+    def reference_init(self, group, prefix):
+        """Consume the CPU generator exactly like mlp(dims, layer_factory) and write the
+        resulting weights into the flat group."""
+        ws = []
+        for i in range(self.n_layers):
+            din, dout = self.dims[i], self.dims[i + 1]
+            if self.E is None:
+                nn.Linear(din, dout)                        # construction-time reset_parameters
+                ws.append(torch.empty(dout, din))
+            else:
+                lin = nn.Linear(din, dout)                  # BatchedLinear.reset_parameters
+                for _ in range(self.E):
+                    lin.reset_parameters()
+                ws.append(torch.empty(self.E, dout, din))
+        for i, w in enumerate(ws):                          # net.apply(weight_initializer())
+            nn.init.xavier_normal_(w)
+            group.view(f'{prefix}{2 * i}.weight').copy_(w)
+            group.view(f'{prefix}{2 * i}.bias').zero_()
+
+
+def layer_views(group, prefix, spec, buf=None):
+    """[(W, b)] views for each Linear of an MLP stored under prefix."""
+    return [(group.view(f'{prefix}{2 * i}.weight', buf), group.view(f'{prefix}{2 * i}.bias', buf))
+            for i in range(spec.n_layers)]

@@ -1,0 +1,49 @@
+"""Tanh-squashed diagonal Gaussian policy (src/policy.py:61-100, src/squashed_gaussian.py).
+
+The MLP S->H..->2A (ReLU) lives in a flat parameter group; ``act`` runs the fused
+HIP MLP forward + squashed-Gaussian head (see ops.py)."""
+import torch
+
+from .params import FlatGroup, MLPSpec
+from .torch_util import Module
+
+
+class SquashedGaussianPolicy(Module):
+    def __init__(self, state_dim, action_dim, hidden_dim=256, hidden_layers=2, group=None, prefix='net.',
+                 log_std_bounds=(-6, 4), std_multiplier=1.0):
+        super().__init__()
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.spec = MLPSpec([state_dim, *([hidden_dim] * hidden_layers), 2 * action_dim], 'relu')
+        self.log_std_bounds = log_std_bounds
+        self.std_multiplier = std_multiplier
+        assert tuple(log_std_bounds) == (-6, 4) and std_multiplier == 1.0, \
+            'the fused head implements the reference defaults log_std_bounds=(-6,4), std_multiplier=1'
+        self.group = group
+        self.prefix = prefix
+
+    @classmethod
+    def create(cls, state_dim, action_dim, hidden_dim, hidden_layers, name, device, init=True):
+        g = FlatGroup(name)
+        pol = cls(state_dim, action_dim, hidden_dim, hidden_layers, group=g)
+        pol.spec.register(g, 'net.')
+        g.allocate('cpu')
+        if init:
+            pol.spec.reference_init(g, 'net.')
+        g.data = g.data.to(device)
+        g.grad = g.grad.to(device)
+        pol.net = pol.spec.build(g, 'net.')
+        return pol
+
+    def layers(self, buf=None):
+        from .params import layer_views
+        return layer_views(self.group, 'net.', self.spec, buf)
+
+    def act(self, states, eval):
+        from . import ops
+        return ops.policy_act(self, states, eval)
+
+    def act1(self, state, eval=False):
+        return self.act(torch.unsqueeze(state, 0), eval)[0]
+
+    def copy_from(self, other):
+        self.group.data.copy_(other.group.data)

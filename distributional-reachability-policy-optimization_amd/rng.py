@@ -1,0 +1,100 @@
+"""Noise sources for the hot path.
+
+Production: ``DeviceNoise`` -- kernels draw Philox4x32-10 normals / uniforms on
+the device from (seed, per-call counter, call-site id); host-RNG choices the
+reference makes on the host (elite member per rollout step, critic pick) keep
+using Python's ``random`` like the reference.
+
+Parity mode: ``TapeNoise`` -- replays a recorded draw sequence (the format of
+tests/golden/tape.py) in the reference's call order, so the HIP path consumes
+exactly the random numbers the reference consumed (noise injection).
+"""
+import random
+
+import numpy as np
+
+
+class DeviceNoise:
+    parity = False
+
+    def __init__(self, seed=0):
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.ctr = 0
+
+    def next(self):
+        self.ctr += 1
+        return self.ctr
+
+    # reference host-RNG call sites
+    def choice(self, n):
+        return random.choice(range(n))
+
+    # device-drawn sites: nothing to hand over
+    def np_choice(self, high, size):
+        return None
+
+    def normal(self, shape):
+        return None
+
+    def std_normal(self, shape):
+        return None
+
+    def randn_like(self, shape, used=True):
+        return None
+
+    def randint(self, high, n):
+        return None
+
+
+class TapeNoise:
+    parity = True
+
+    def __init__(self, entries):
+        self.entries = list(entries)
+        self.pos = 0
+        self.seed, self.ctr = 0, 0
+
+    @classmethod
+    def from_npz(cls, d, prefix):
+        n = int(d[f'{prefix}_n'])
+        keys = sorted(k for k in d.files if k.startswith(prefix + '_') and k != f'{prefix}_n')
+        assert len(keys) == n
+        return cls([(k[len(prefix) + 6:], d[k]) for k in keys])
+
+    def next(self):
+        return 0
+
+    def peek(self):
+        return self.entries[self.pos][0] if self.pos < len(self.entries) else None
+
+    def _take(self, kind, shape=None):
+        if self.pos >= len(self.entries):
+            raise AssertionError(f'noise tape exhausted (wanted {kind})')
+        k, v = self.entries[self.pos]
+        if k != kind:
+            raise AssertionError(f'noise tape position {self.pos}: expected {kind}, found {k}')
+        if shape is not None and tuple(v.shape) != tuple(shape):
+            raise AssertionError(f'noise tape {kind} shape {v.shape} != {tuple(shape)}')
+        self.pos += 1
+        return v
+
+    def choice(self, n):
+        return int(self._take('choice'))
+
+    def np_choice(self, high, size):
+        return np.asarray(self._take('np_choice', (size,)), dtype=np.int64)
+
+    def normal(self, shape):
+        return np.ascontiguousarray(self._take('normal', shape), dtype=np.float32)
+
+    def std_normal(self, shape):
+        return np.ascontiguousarray(self._take('normal_', shape), dtype=np.float32)
+
+    def randn_like(self, shape, used=True):
+        return np.ascontiguousarray(self._take('randn_like', shape), dtype=np.float32)
+
+    def randint(self, high, n):
+        return np.asarray(self._take('randint', (n,)), dtype=np.int64)
+
+    def done(self):
+        return self.pos == len(self.entries)
