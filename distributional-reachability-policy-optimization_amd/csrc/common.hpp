@@ -138,56 +138,15 @@ __device__ __forceinline__ f32x4 load_w4(const float* __restrict__ W, int ldw, i
 // so it stays in VGPRs.
 constexpr int PF_D = 4;
 
-template <int RB, int MAXC, int ACT, bool VEC>
-__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
-                                                const float* __restrict__ bias, int N, float* out, int ldo) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+template <int NW, int RB, int MAXC, int ACT>
+__device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], const float* __restrict__ bias, int N,
+                                               float* out, int ldo) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l15 = lane & 15, g = lane >> 4;
   const int NB = (N + 15) >> 4;
-
-  f32x4 acc[RB][MAXC];
-#pragma unroll
-  for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  f32x4 bq[PF_D][MAXC];
-#pragma unroll
-  for (int u = 0; u < PF_D - 1; ++u)
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      const int cb = wave + 4 * c;
-      bq[u][c] = load_w4<VEC>(W, ldw, cb * 16 + l15, 16 * u + 4 * g, N, K);
-    }
-  for (int kb = 0; kb < K; kb += 16 * PF_D) {
-#pragma unroll
-    for (int u = 0; u < PF_D; ++u) {
-      const int k0 = kb + 16 * u;
-      const int kl = k0 + 16 * (PF_D - 1);
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c) {
-        const int cb = wave + 4 * c;
-        bq[(u + PF_D - 1) % PF_D][c] = load_w4<VEC>(W, ldw, cb * 16 + l15, kl + 4 * g, N, K);
-      }
-      if (k0 < K) {
-        f32x4 a[RB];
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-          a[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int c = 0; c < MAXC; ++c)   // out-of-range column blocks compute discarded values
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb)
-              acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][m], bq[u][c][m], acc[rb][c], 0, 0, 0);
-      }
-    }
-  }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int cb = wave + 4 * c;
+    const int cb = wave + NW * c;
     if (cb >= NB) continue;
     const int col = cb * 16 + l15;
     const float bv = (col < N && bias) ? bias[col] : 0.f;
@@ -201,26 +160,181 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
   }
 }
 
+// One layer for an RB*16-row tile by NW waves (NW*64 threads); wave w owns the
+// 16-column blocks w, w+NW, ... (MAXC of them).
+// NK > 0: compile-time number of 16-deep k-steps -> fully unrolled, so the weight
+// ring and the one-step-ahead LDS A prefetch are indexed statically and the
+// compiler's vmcnt accounting never has to cross a loop back-edge (a back-edge
+// forces vmcnt(0), collapsing the prefetch distance). NK == 0: runtime K loop.
+template <int NW, int RB, int MAXC, int ACT, bool VEC, int NK>
+__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
+                                                const float* __restrict__ bias, int N, float* out, int ldo) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+
+  f32x4 acc[RB][MAXC];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 bq[PF_D][MAXC];
+#pragma unroll
+  for (int u = 0; u < PF_D - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      bq[u][c] = load_w4<VEC>(W, ldw, (wave + NW * c) * 16 + l15, 16 * u + 4 * g, N, K);
+
+  if constexpr (NK > 0) {
+    f32x4 an[RB], ac[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      if (s + PF_D - 1 < NK) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+          bq[(s + PF_D - 1) % PF_D][c] =
+              load_w4<VEC>(W, ldw, (wave + NW * c) * 16 + l15, 16 * (s + PF_D - 1) + 4 * g, N, K);
+      }
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
+      if (s + 1 < NK) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 16 * (s + 1) + 4 * g);
+      }
+      // keep the prefetches where they are: without this fence the scheduler sinks
+      // them next to their consumers and the ring degenerates to distance 1
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+            acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF_D][c][m], acc[rb][c], 0, 0, 0);
+    }
+  } else {
+    for (int kb = 0; kb < K; kb += 16 * PF_D) {
+#pragma unroll
+      for (int u = 0; u < PF_D; ++u) {
+        const int k0 = kb + 16 * u;
+        const int kl = k0 + 16 * (PF_D - 1);
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+          bq[(u + PF_D - 1) % PF_D][c] = load_w4<VEC>(W, ldw, (wave + NW * c) * 16 + l15, kl + 4 * g, N, K);
+        if (k0 < K) {
+          f32x4 a[RB];
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+            a[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c)   // out-of-range column blocks compute discarded values
+#pragma unroll
+              for (int rb = 0; rb < RB; ++rb)
+                acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][m], bq[u][c][m], acc[rb][c], 0, 0, 0);
+        }
+      }
+    }
+  }
+  dense_epilogue<NW, RB, MAXC, ACT>(acc, bias, N, out, ldo);
+}
+
+template <int NW, int RB, int MAXC, int ACT, bool VEC>
+__device__ __forceinline__ void tile_dense_nk(const float* in, int ldi, int K, const float* W, int ldw,
+                                              const float* bias, int N, float* out, int ldo) {
+  switch ((K + 15) >> 4) {
+    case 1: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 1>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    case 13: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 13>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    case 16: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 16>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    default: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 0>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+  }
+}
+
 // Row-aligned fast path (float4 weight loads) when K % 4 == 0, else scalar loads.
-template <int RB, int MAXC, int ACT>
+// MAXC = column blocks per wave: ceil(ceil(N/16)/NW) must be <= MAXC.
+template <int NW, int RB, int MAXC, int ACT>
 __device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
                                            const float* __restrict__ bias, int N, float* out, int ldo) {
   if ((ldw & 3) == 0 && (K & 3) == 0)
-    tile_dense_impl<RB, MAXC, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo);
+    tile_dense_nk<NW, RB, MAXC, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo);
   else
-    tile_dense_impl<RB, MAXC, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo);
+    tile_dense_nk<NW, RB, MAXC, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo);
 }
 
-// Dispatch on a runtime activation id.
-template <int RB, int MAXC>
-__device__ __forceinline__ void tile_dense_act(int act, const float* in, int ldi, int K, const float* W, int ldw,
-                                               const float* bias, int N, float* out, int ldo) {
-  switch (act) {
-    case ACT_RELU: tile_dense<RB, MAXC, ACT_RELU>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
-    case ACT_SILU: tile_dense<RB, MAXC, ACT_SILU>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
-    case ACT_TANH: tile_dense<RB, MAXC, ACT_TANH>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
-    default: tile_dense<RB, MAXC, ACT_NONE>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+// Narrow layer (N <= 16, one column block): the K reduction is split over the NW
+// waves (k-steps s == wave mod NW), partial 16x16 tiles are summed through LDS
+// (`red`: NW*RB*256 floats), then bias + activation. Avoids one wave doing the
+// whole narrow head serially while the others idle.
+template <int NW, int RB, int ACT, bool VEC>
+__device__ __forceinline__ void tile_dense_narrow_impl(const float* in, int ldi, int K, const float* __restrict__ W,
+                                                       int ldw, const float* __restrict__ bias, int N, float* out,
+                                                       int ldo, float* red) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NKS = (K + 15) >> 4;
+  f32x4 acc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // each wave: at most ceil(16/NW) k-steps for K <= 256; issue all loads first
+  constexpr int MAXS = (16 + NW - 1) / NW;
+  f32x4 b[MAXS], a[MAXS][RB];
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    const int s = wave + NW * q;
+    const int k0 = (s < NKS ? s : 0) * 16;
+    b[q] = load_w4<VEC>(W, ldw, l15, k0 + 4 * g, N, K);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
   }
+  for (int kb = NW * MAXS; kb < NKS; kb += NW) {   // K > 16*NW*MAXS (only for K > 256)
+    const int k0 = (kb + wave) * 16;
+    if (kb + wave < NKS) {
+      const f32x4 bb = load_w4<VEC>(W, ldw, l15, k0 + 4 * g, N, K);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const f32x4 aa = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[m], bb[m], acc[rb], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    if (wave + NW * q < NKS) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][rb][m], b[q][m], acc[rb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+  __syncthreads();
+  for (int e = tid; e < RB * 256; e += NW * 64) {
+    const int rb = e >> 8, rr = (e >> 4) & 15, col = e & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[(w * RB + rb) * 256 + rr * 16 + col];
+    out[(rb * 16 + rr) * ldo + col] = (col < N) ? act_fn<ACT>(v + (bias ? bias[col < N ? col : 0] : 0.f)) : 0.f;
+  }
+}
+
+template <int NW, int RB, int ACT>
+__device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int K, const float* W, int ldw,
+                                                  const float* bias, int N, float* out, int ldo, float* red) {
+  if ((ldw & 3) == 0 && (K & 3) == 0)
+    tile_dense_narrow_impl<NW, RB, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo, red);
+  else
+    tile_dense_narrow_impl<NW, RB, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo, red);
 }
 
 }  // namespace drpo

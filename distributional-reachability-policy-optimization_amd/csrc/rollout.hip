@@ -1,7 +1,7 @@
 // Fused imagined-rollout step (SMBPO.rollout, src/smbpo.py:229-249).
 //
 // One launch of rollout_step_kernel processes one horizon step for every alive
-// row: each 256-thread workgroup owns a 16- or 32-row tile and keeps all of its
+// row: each 512-thread workgroup (8 wave64s, 2 per SIMD) owns a 16- or 32-row tile and keeps all of its
 // activations in LDS while it runs
 //   actor MLP S->H->H->2A (ReLU)  +  squashed-Gaussian sample   (src/policy.py:89-97)
 //   elite member MLP trunk/diff/log-var heads (SiLU) + log-var clamp + Gaussian
@@ -91,9 +91,11 @@ __device__ inline int64_t prp_index(uint64_t i, uint64_t N, int hb, const uint32
   return (int64_t)(x % N);   // unreachable in practice (expected walk < 4)
 }
 
-template <int RB>
-__global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
+template <int RB, int NW>
+__global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p) {
   constexpr int ROWS = RB * 16;
+  constexpr int NT = NW * 64;                   // 2 waves per SIMD at NW = 8
+  constexpr int MAXC = (16 + NW - 1) / NW;      // column blocks per wave for widths <= 256
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int S = p.S, A = p.A, C = p.C, S1 = p.S + 1;
@@ -110,8 +112,9 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
   float* hval = rew + ROWS;                // ROWS x 8    constraint values
   int* flags = reinterpret_cast<int*>(hval + ROWS * 8);   // ROWS: bit0 done, bit1 violation
   int* srcrow = flags + ROWS;                              // ROWS
-  int* s_part = srcrow + ROWS;                             // 256 scan partials
-  int* scan = s_part + 256;                                // prev tiles + 1 (exclusive prefix)
+  float* red = reinterpret_cast<float*>(srcrow + ROWS);    // NW*RB*256 narrow-layer partials
+  int* s_part = reinterpret_cast<int*>(red + NW * RB * 256);   // NT scan partials
+  int* scan = s_part + NT;                                 // prev tiles + 1 (exclusive prefix)
 
   // ---- 0. row count / buffer offset of this step + compaction map ----------
   int n;
@@ -123,8 +126,8 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
   } else {
     const int n_prev = p.n[p.t - 1];
     const int T = (n_prev + ROWS - 1) / ROWS;
-    // exclusive scan of the previous step's tile counts (T <= ntiles), 256 threads
-    const int per = (T + 255) / 256;
+    // exclusive scan of the previous step's tile counts (T <= ntiles), NT threads
+    const int per = (T + NT - 1) / NT;
     const int b0 = tid * per;
     int run = 0;
     for (int i = 0; i < per; ++i) {
@@ -136,23 +139,24 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
     }
     s_part[tid] = run;
     __syncthreads();
-    if (tid < 64) {   // exclusive scan of the 256 partials in one wave
-      int v[4], sum = 0;
-      for (int q = 0; q < 4; ++q) { v[q] = s_part[tid * 4 + q]; sum += v[q]; }
+    if (tid < 64) {   // exclusive scan of the NT partials in one wave
+      constexpr int PPL = NT / 64;
+      int v[PPL], sum = 0;
+      for (int q = 0; q < PPL; ++q) { v[q] = s_part[tid * PPL + q]; sum += v[q]; }
       int incl = sum;
       for (int o = 1; o < 64; o <<= 1) {
         const int y = __shfl_up(incl, o, 64);
         if (tid >= o) incl += y;
       }
       int e = incl - sum;
-      for (int q = 0; q < 4; ++q) { const int x = v[q]; s_part[tid * 4 + q] = e; e += x; }
+      for (int q = 0; q < PPL; ++q) { const int x = v[q]; s_part[tid * PPL + q] = e; e += x; }
     }
     __syncthreads();
     for (int i = 0; i < per; ++i) {
       const int ti = b0 + i;
       if (ti < T) scan[ti] += s_part[tid];
     }
-    if (tid == 255) scan[T] = s_part[255] + run;    // total alive == n for this step
+    if (tid == NT - 1) scan[T] = s_part[NT - 1] + run;    // total alive == n for this step
     __syncthreads();
     n = scan[T];
     off = p.off[p.t - 1] + n_prev;
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
 
   // ---- 1. gather the tile's states (zero-padded) ---------------------------
   const int kpad = round_up(S + A, 16);
-  for (int e = tid; e < ROWS * kpad; e += WG) {
+  for (int e = tid; e < ROWS * kpad; e += NT) {
     const int r = e / kpad, k = e - r * kpad;
     float v = 0.f;
     if (r < rows && k < S) {
@@ -196,15 +200,15 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
   __syncthreads();
 
   // ---- 2. actor MLP (src/policy.py:61-100; mlp() ReLU hidden) ---------------
-  tile_dense<RB, 4, ACT_RELU>(xin, p.ldx, S, p.aW1, S, p.ab1, p.Ha, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_RELU>(xin, p.ldx, S, p.aW1, S, p.ab1, p.Ha, h1, p.ldh);
   __syncthreads();
-  tile_dense<RB, 4, ACT_RELU>(h1, p.ldh, p.Ha, p.aW2, p.Ha, p.ab2, p.Ha, h2, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_RELU>(h1, p.ldh, p.Ha, p.aW2, p.Ha, p.ab2, p.Ha, h2, p.ldh);
   __syncthreads();
-  tile_dense<RB, 1, ACT_NONE>(h2, p.ldh, p.Ha, p.aW3, p.Ha, p.ab3, 2 * A, ao, 20);
+  tile_dense_narrow<NW, RB, ACT_NONE>(h2, p.ldh, p.Ha, p.aW3, p.Ha, p.ab3, 2 * A, ao, 20, red);
   __syncthreads();
 
   // ---- 3. squashed Gaussian sample + model input [normalize(s), a] ----------
-  for (int e = tid; e < ROWS * A; e += WG) {
+  for (int e = tid; e < ROWS * A; e += NT) {
     const int r = e / A, d = e - r * A;
     const float mu = ao[r * 20 + d], raw = ao[r * 20 + A + d];
     const float ls = -6.f + 10.f * sigmoidf(raw);
@@ -221,28 +225,30 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
     act[r * 8 + d] = a;
     xin[r * p.ldx + S + d] = a;
   }
-  for (int e = tid; e < ROWS * S; e += WG) {
+  for (int e = tid; e < ROWS * S; e += NT) {
     const int r = e / S, k = e - r * S;
     xin[r * p.ldx + k] = (sraw[r * p.lds + k] - p.norm_mean[k]) / (p.norm_std[k] + 1e-6f);
   }
   __syncthreads();
 
   // ---- 4. elite member forward (src/dynamics.py:112-122, swish) -------------
-  tile_dense<RB, 4, ACT_SILU>(xin, p.ldx, S + A, p.mW1, S + A, p.mb1, p.Hm, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(xin, p.ldx, S + A, p.mW1, S + A, p.mb1, p.Hm, h1, p.ldh);
   __syncthreads();
-  tile_dense<RB, 4, ACT_SILU>(h1, p.ldh, p.Hm, p.mW2, p.Hm, p.mb2, p.Hm, h2, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(h1, p.ldh, p.Hm, p.mW2, p.Hm, p.mb2, p.Hm, h2, p.ldh);
   __syncthreads();
-  tile_dense<RB, 4, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.Hm, p.db1, p.Hm, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.Hm, p.db1, p.Hm, h1, p.ldh);
   __syncthreads();
-  tile_dense<RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.Hm, p.db2, S1, dout, p.ldm);
+  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.Hm, p.db2, S1, dout, p.ldm, red);
+  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.Hm, p.db2, S1, dout, p.ldm);
   __syncthreads();
-  tile_dense<RB, 4, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.Hm, p.lb1, p.Hm, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.Hm, p.lb1, p.Hm, h1, p.ldh);
   __syncthreads();
-  tile_dense<RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.Hm, p.lb2, S1, lout, p.ldm);
+  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.Hm, p.lb2, S1, lout, p.ldm, red);
+  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.Hm, p.lb2, S1, lout, p.ldm);
   __syncthreads();
 
   // ---- 5. residual mean, log-var soft clamp, Gaussian sample ---------------
-  for (int e = tid; e < ROWS * S1; e += WG) {
+  for (int e = tid; e < ROWS * S1; e += NT) {
     const int r = e / S1, j = e - r * S1;
     const float mean = dout[r * p.ldm + j] + (j < S ? sraw[r * p.lds + j] : 0.f);
     float lv = lout[r * p.ldm + j];
@@ -281,7 +287,7 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
   __syncthreads();
 
   // ---- 7. row writes into the circular virtual buffer + next-state scratch --
-  for (int e = tid; e < rows * S; e += WG) {
+  for (int e = tid; e < rows * S; e += NT) {
     const int r = e / S, k = e - r * S;
     const int64_t q = (vbase + r) % p.vcap;
     p.vs[q * S + k] = sraw[r * p.lds + k];
@@ -289,11 +295,11 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(RolloutStepArgs p) {
     p.vs2[q * S + k] = x;
     p.nxt[(int64_t)(row0 + r) * S + k] = x;
   }
-  for (int e = tid; e < rows * A; e += WG) {
+  for (int e = tid; e < rows * A; e += NT) {
     const int r = e / A, d = e - r * A;
     p.va[((vbase + r) % p.vcap) * A + d] = act[r * 8 + d];
   }
-  for (int e = tid; e < rows * C; e += WG) {
+  for (int e = tid; e < rows * C; e += NT) {
     const int r = e / C, c = e - r * C;
     p.vh[((vbase + r) % p.vcap) * C + c] = hval[r * 8 + c];
   }
@@ -441,8 +447,9 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, hipStream_t stream) {
   a.lds = round_up(S, 4);
 
   const int tiles = (d->B + rpt - 1) / rpt;
+  constexpr int NW = 8;
   const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 2 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 2) +
-                                            (size_t)tiles + 1 + 256);
+                                            (size_t)NW * (rpt / 16) * 256 + NW * 64 + (size_t)tiles + 1);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
 
   const int E_out_in[6][2] = {{d->Hm, S + A}, {d->Hm, d->Hm}, {d->Hm, d->Hm}, {S1, d->Hm}, {d->Hm, d->Hm}, {S1, d->Hm}};
@@ -467,9 +474,9 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, hipStream_t stream) {
     a.eps_m = d->eps_m ? d->eps_m + (size_t)t * d->B * S1 : nullptr;
     if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[2 * t], stream);
     if (rpt == 32)
-      rollout_step_kernel<2><<<tiles, 256, lds_bytes, stream>>>(a);
+      rollout_step_kernel<2, NW><<<tiles, NW * 64, lds_bytes, stream>>>(a);
     else
-      rollout_step_kernel<1><<<tiles, 256, lds_bytes, stream>>>(a);
+      rollout_step_kernel<1, NW><<<tiles, NW * 64, lds_bytes, stream>>>(a);
     DRPO_LAUNCH_CHECK("rollout_step");
     if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[2 * t + 1], stream);
   }
