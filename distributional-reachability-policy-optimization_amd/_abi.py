@@ -57,3 +57,78 @@ def declare(lib):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+
+
+class MlpLayer(ctypes.Structure):
+    """drpo_mlp_layer_t"""
+    _fields_ = [('W', P), ('b', P), ('din', c_int), ('dout', c_int), ('act', c_int), ('sy', P), ('sz', P),
+                ('wstride', c_int64), ('bstride', c_int64)]
+
+
+class MlpNet(ctypes.Structure):
+    _fields_ = [('nl', c_int), ('L', MlpLayer * 3)]
+
+
+class MlpFwd(ctypes.Structure):
+    """drpo_mlp_fwd_t"""
+    _fields_ = [('src', P * 3), ('cols', c_int * 3), ('ld', c_int * 3), ('sstride', c_int64 * 3),
+                ('nmean', P), ('nstd', P), ('save_x', P), ('net', MlpNet * 3), ('nnets', c_int), ('trunk', c_int),
+                ('rows', c_int64), ('nbatch', c_int)]
+
+
+class MlpBwdLayer(ctypes.Structure):
+    """drpo_mlp_bwd_layer_t"""
+    _fields_ = [('W', P), ('din', c_int), ('dout', c_int), ('act', c_int), ('sy', P), ('sz', P), ('dz', P),
+                ('wstride', c_int64)]
+
+
+class MlpBwdNet(ctypes.Structure):
+    _fields_ = [('nl', c_int), ('L', MlpBwdLayer * 3), ('gout', P), ('dx', P), ('dx_col0', c_int),
+                ('dx_cols', c_int), ('dx_accumulate', c_int)]
+
+
+class MlpBwd(ctypes.Structure):
+    """drpo_mlp_bwd_t"""
+    _fields_ = [('net', MlpBwdNet * 3), ('nnets', c_int), ('trunk', c_int), ('rows', c_int64), ('nbatch', c_int)]
+
+
+class WgradItem(ctypes.Structure):
+    """drpo_wgrad_item_t"""
+    _fields_ = [('dz', P), ('y', P), ('gW', P), ('gb', P), ('dout', c_int), ('din', c_int), ('rows', c_int64),
+                ('zstride', c_int64), ('ystride', c_int64), ('gwstride', c_int64), ('gbstride', c_int64),
+                ('nbatch', c_int)]
+
+
+class BufferView(ctypes.Structure):
+    """drpo_buffer_view_t"""
+    _fields_ = [('s', P), ('a', P), ('s2', P), ('r', P), ('h', P), ('d', P), ('v', P), ('len', c_int64),
+                ('ptr_dev', P), ('cap', c_int64)]
+
+
+class CriticHead(ctypes.Structure):
+    """drpo_critic_head_t"""
+    _fields_ = [('B', c_int64), ('C', c_int), ('distributional', c_int), ('deterministic_backup', c_int),
+                ('discount', c_float), ('qc_td_bound', c_float), ('lmin', c_float), ('lmax', c_float),
+                ('log_alpha', P), ('r', P), ('h', P), ('d', P), ('q0t', P), ('q1t', P), ('logp2', P),
+                ('mu_t', P), ('ls_t', P), ('eps3', P), ('seed', c_uint64), ('ctr', c_uint64),
+                ('q0', P), ('q1', P), ('mu', P), ('ls', P), ('dq0', P), ('dq1', P), ('dmu', P), ('dls', P),
+                ('loss', P)]
+
+
+PROTOTYPES.update({
+    'drpo_mlp_forward': (c_int, [POINTER(MlpFwd), P]),
+    'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
+    'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P]),
+    'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
+                                  c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
+    'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,
+                                 P]),
+    'drpo_cc_head': (c_int, [P, P, c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P]),
+    'drpo_critic_head': (c_int, [POINTER(CriticHead), P]),
+    'drpo_actor_upstream': (c_int, [c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P, P, P, P, P, P, P, P,
+                                    P]),
+    'drpo_squash_backward': (c_int, [c_int64, c_int, P, P, P, P, P, c_float, P, c_float, P, P, P]),
+    'drpo_alpha_grad': (c_int, [P, P, c_int64, P, P]),
+    'drpo_multiplier_head': (c_int, [c_int64, P, P, P, c_float, c_float, c_float, c_float, c_float, P, P, P]),
+    'drpo_multiplier_out': (c_int, [c_int64, P, c_float, P, P]),
+})

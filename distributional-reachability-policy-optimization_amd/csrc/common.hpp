@@ -138,9 +138,18 @@ __device__ __forceinline__ f32x4 load_w4(const float* __restrict__ W, int ldw, i
 // so it stays in VGPRs.
 constexpr int PF_D = 4;
 
+// Optional global saves of the tile (rows < nrows only): gy = post-activation,
+// gz = pre-activation, row stride ldg (already offset to the tile's first row).
+struct GSave {
+  float* gy;
+  float* gz;
+  int ldg;
+  int nrows;
+};
+
 template <int NW, int RB, int MAXC, int ACT>
 __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], const float* __restrict__ bias, int N,
-                                               float* out, int ldo) {
+                                               float* out, int ldo, const GSave& gs) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l15 = lane & 15, g = lane >> 4;
   const int NB = (N + 15) >> 4;
@@ -155,9 +164,25 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rb * 16 + 4 * g + r;
-        out[row * ldo + col] = (col < N) ? act_fn<ACT>(acc[rb][c][r] + bv) : 0.f;
+        const float z = acc[rb][c][r] + bv;
+        const float y = act_fn<ACT>(z);
+        if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
+        if (col < N && row < gs.nrows) {
+          if (gs.gy) gs.gy[(size_t)row * gs.ldg + col] = y;
+          if (gs.gz) gs.gz[(size_t)row * gs.ldg + col] = z;
+        }
       }
   }
+}
+
+// B fragment of the TRANSPOSED weight: lane (col n, group g) gets W[kk+i][n],
+// i = 0..3 (W row-major [K][ldw]); used by backward-data products dY = dZ * W.
+__device__ __forceinline__ f32x4 load_wT4(const float* __restrict__ W, int ldw, int n, int kk, int N, int K) {
+  const int nc = n < N ? n : N - 1;
+  f32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = W[(size_t)(kk + i < K ? kk + i : K - 1) * ldw + nc];
+  return r;
 }
 
 // One layer for an RB*16-row tile by NW waves (NW*64 threads); wave w owns the
@@ -166,9 +191,11 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
 // ring and the one-step-ahead LDS A prefetch are indexed statically and the
 // compiler's vmcnt accounting never has to cross a loop back-edge (a back-edge
 // forces vmcnt(0), collapsing the prefetch distance). NK == 0: runtime K loop.
-template <int NW, int RB, int MAXC, int ACT, bool VEC, int NK>
+template <int NW, int RB, int MAXC, int ACT, bool VEC, int NK, bool TRANS = false>
 __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
-                                                const float* __restrict__ bias, int N, float* out, int ldo) {
+                                                const float* __restrict__ bias, int N, float* out, int ldo,
+                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+#define DRPO_LOADB(col, kk) (TRANS ? load_wT4(W, ldw, (col), (kk), N, K) : load_w4<VEC>(W, ldw, (col), (kk), N, K))
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -184,7 +211,7 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
   for (int u = 0; u < PF_D - 1; ++u)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
-      bq[u][c] = load_w4<VEC>(W, ldw, (wave + NW * c) * 16 + l15, 16 * u + 4 * g, N, K);
+      bq[u][c] = DRPO_LOADB((wave + NW * c) * 16 + l15, 16 * u + 4 * g);
 
   if constexpr (NK > 0) {
     f32x4 an[RB], ac[RB];
@@ -195,8 +222,7 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
       if (s + PF_D - 1 < NK) {
 #pragma unroll
         for (int c = 0; c < MAXC; ++c)
-          bq[(s + PF_D - 1) % PF_D][c] =
-              load_w4<VEC>(W, ldw, (wave + NW * c) * 16 + l15, 16 * (s + PF_D - 1) + 4 * g, N, K);
+          bq[(s + PF_D - 1) % PF_D][c] = DRPO_LOADB((wave + NW * c) * 16 + l15, 16 * (s + PF_D - 1) + 4 * g);
       }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
@@ -224,7 +250,7 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
         const int kl = k0 + 16 * (PF_D - 1);
 #pragma unroll
         for (int c = 0; c < MAXC; ++c)
-          bq[(u + PF_D - 1) % PF_D][c] = load_w4<VEC>(W, ldw, (wave + NW * c) * 16 + l15, kl + 4 * g, N, K);
+          bq[(u + PF_D - 1) % PF_D][c] = DRPO_LOADB((wave + NW * c) * 16 + l15, kl + 4 * g);
         if (k0 < K) {
           f32x4 a[RB];
 #pragma unroll
@@ -241,17 +267,19 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
       }
     }
   }
-  dense_epilogue<NW, RB, MAXC, ACT>(acc, bias, N, out, ldo);
+  dense_epilogue<NW, RB, MAXC, ACT>(acc, bias, N, out, ldo, gs);
+#undef DRPO_LOADB
 }
 
-template <int NW, int RB, int MAXC, int ACT, bool VEC>
+template <int NW, int RB, int MAXC, int ACT, bool VEC, bool TRANS = false>
 __device__ __forceinline__ void tile_dense_nk(const float* in, int ldi, int K, const float* W, int ldw,
-                                              const float* bias, int N, float* out, int ldo) {
+                                              const float* bias, int N, float* out, int ldo,
+                                              const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
   switch ((K + 15) >> 4) {
-    case 1: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 1>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
-    case 13: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 13>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
-    case 16: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 16>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
-    default: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 0>(in, ldi, K, W, ldw, bias, N, out, ldo); break;
+    case 1: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 1, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
+    case 13: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 13, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
+    case 16: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 16, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
+    default: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 0, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
   }
 }
 
@@ -259,11 +287,19 @@ __device__ __forceinline__ void tile_dense_nk(const float* in, int ldi, int K, c
 // MAXC = column blocks per wave: ceil(ceil(N/16)/NW) must be <= MAXC.
 template <int NW, int RB, int MAXC, int ACT>
 __device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
-                                           const float* __restrict__ bias, int N, float* out, int ldo) {
+                                           const float* __restrict__ bias, int N, float* out, int ldo,
+                                           const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
   if ((ldw & 3) == 0 && (K & 3) == 0)
-    tile_dense_nk<NW, RB, MAXC, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo);
+    tile_dense_nk<NW, RB, MAXC, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo, gs);
   else
-    tile_dense_nk<NW, RB, MAXC, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo);
+    tile_dense_nk<NW, RB, MAXC, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo, gs);
+}
+
+// out[r][n] = sum_k in[r][k] * W[k][n] (W row-major [K][ldw]): backward-data product.
+template <int NW, int RB, int MAXC>
+__device__ __forceinline__ void tile_dense_T(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
+                                             int N, float* out, int ldo) {
+  tile_dense_nk<NW, RB, MAXC, ACT_NONE, false, true>(in, ldi, K, W, ldw, nullptr, N, out, ldo);
 }
 
 // Narrow layer (N <= 16, one column block): the K reduction is split over the NW
@@ -273,7 +309,7 @@ __device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, cons
 template <int NW, int RB, int ACT, bool VEC>
 __device__ __forceinline__ void tile_dense_narrow_impl(const float* in, int ldi, int K, const float* __restrict__ W,
                                                        int ldw, const float* __restrict__ bias, int N, float* out,
-                                                       int ldo, float* red) {
+                                                       int ldo, float* red, const GSave& gs) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -324,17 +360,25 @@ __device__ __forceinline__ void tile_dense_narrow_impl(const float* in, int ldi,
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[(w * RB + rb) * 256 + rr * 16 + col];
-    out[(rb * 16 + rr) * ldo + col] = (col < N) ? act_fn<ACT>(v + (bias ? bias[col < N ? col : 0] : 0.f)) : 0.f;
+    const float z = v + (bias ? bias[col < N ? col : 0] : 0.f);
+    const float y = act_fn<ACT>(z);
+    const int row = rb * 16 + rr;
+    if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
+    if (col < N && row < gs.nrows) {
+      if (gs.gy) gs.gy[(size_t)row * gs.ldg + col] = y;
+      if (gs.gz) gs.gz[(size_t)row * gs.ldg + col] = z;
+    }
   }
 }
 
 template <int NW, int RB, int ACT>
 __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int K, const float* W, int ldw,
-                                                  const float* bias, int N, float* out, int ldo, float* red) {
+                                                  const float* bias, int N, float* out, int ldo, float* red,
+                                                  const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
   if ((ldw & 3) == 0 && (K & 3) == 0)
-    tile_dense_narrow_impl<NW, RB, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo, red);
+    tile_dense_narrow_impl<NW, RB, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo, red, gs);
   else
-    tile_dense_narrow_impl<NW, RB, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo, red);
+    tile_dense_narrow_impl<NW, RB, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo, red, gs);
 }
 
 }  // namespace drpo

@@ -1,0 +1,484 @@
+// Generic fused MLP kernels for the SAC update and the ensemble fit (mlp() nets of
+// src/torch_util.py:190-211; BatchedLinear ensembles of src/dynamics.py:26-52).
+//
+//  mlp_fwd_kernel   one launch runs a whole net (or a trunk + its heads) for a
+//                   16-row tile per 512-thread workgroup, activations kept in
+//                   LDS, optional saves of every layer's post-(and pre-)activation
+//                   for the backward pass. grid.y = independent nets on the same
+//                   input (twin critics), grid.z = ensemble members.
+//  mlp_bwd_kernel   fused backward-data: dZ_l = dY_l * act'(saved), dY_{l-1} =
+//                   dZ_l W_l through every layer (heads -> summed trunk grad ->
+//                   trunk), saving dZ_l for the weight gradients and the input
+//                   gradient (e.g. dQ/da for the actor update).
+//  mlp_wgrad_kernel grouped dW = dZ^T Y (+ bias via a ones column) over all layers
+//                   of a parameter group in one launch, 64x64 output tiles x row
+//                   chunks, fp32 MFMA, atomically accumulated into the flat grad.
+#include "common.hpp"
+
+using namespace drpo;
+
+namespace {
+
+constexpr int FW_NW = 8;              // waves per workgroup (fwd / bwd)
+constexpr int FW_NT = FW_NW * 64;
+constexpr int FW_ROWS = 16;
+constexpr int FW_MAXC = 2;            // 16 column blocks / 8 waves
+constexpr int LDH = 264;              // LDS stride for widths <= 256 (== 8 mod 64)
+constexpr int MAXL = 3;
+constexpr int MAXN = 3;
+
+}  // namespace
+
+extern "C" {
+typedef struct {
+  const float* W;        // [dout][din] (member 0 when batched)
+  const float* b;        // [dout]
+  int din, dout, act;
+  float* sy;             // optional save of post-activation [rows][dout] (per batch item)
+  float* sz;             // optional save of pre-activation
+  int64_t wstride, bstride;   // batch (ensemble member) strides in floats
+} drpo_mlp_layer_t;
+
+typedef struct {
+  int nl;
+  drpo_mlp_layer_t L[3];
+} drpo_mlp_net_t;
+
+typedef struct {
+  const float* src[3];   // column-concatenated input sources
+  int cols[3];
+  int ld[3];
+  int64_t sstride[3];    // batch strides (floats)
+  const float* nmean;    // optional normalisation (x - mean) / (std + 1e-6) of src[0]
+  const float* nstd;
+  float* save_x;         // optional save of the assembled input [rows][din0]
+  drpo_mlp_net_t net[3];
+  int nnets;
+  int trunk;             // 1: net[0] is a trunk, net[1..] heads on its output
+  int64_t rows;          // rows per batch item
+  int nbatch;
+} drpo_mlp_fwd_t;
+
+typedef struct {
+  const float* W;
+  int din, dout, act;
+  const float* sy;       // saved post-activation (ReLU / tanh derivative)
+  const float* sz;       // saved pre-activation (SiLU derivative)
+  float* dz;             // optional save of dL/dZ [rows][dout] for weight grads
+  int64_t wstride;
+} drpo_mlp_bwd_layer_t;
+
+typedef struct {
+  int nl;
+  drpo_mlp_bwd_layer_t L[3];
+  const float* gout;     // dL/d(net output) [rows][dout_last]
+  float* dx;             // optional dL/d(net input) columns [dx_col0, dx_col0 + dx_cols) -> [rows][dx_cols]
+  int dx_col0, dx_cols, dx_accumulate;
+} drpo_mlp_bwd_net_t;
+
+typedef struct {
+  drpo_mlp_bwd_net_t net[3];
+  int nnets;
+  int trunk;             // 1: net[0] trunk; heads' input grads are summed into the trunk output grad
+  int64_t rows;
+  int nbatch;
+} drpo_mlp_bwd_t;
+
+typedef struct {
+  const float* dz;       // [rows][dout]
+  const float* y;        // layer input [rows][din]
+  float* gW;             // [dout][din] (+ member stride)
+  float* gb;             // [dout]
+  int dout, din;
+  int64_t rows;
+  int64_t zstride, ystride, gwstride, gbstride;   // batch strides
+  int nbatch;
+} drpo_wgrad_item_t;
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int ACT>
+__device__ __forceinline__ void run_layer_act(const float* in, int ldi, const drpo_mlp_layer_t& L, const float* W,
+                                              const float* b, float* out, int ldo, float* red, const GSave& gs) {
+  if (L.dout <= 16)
+    tile_dense_narrow<FW_NW, 1, ACT>(in, ldi, L.din, W, L.din, b, L.dout, out, ldo, red, gs);
+  else
+    tile_dense<FW_NW, 1, FW_MAXC, ACT>(in, ldi, L.din, W, L.din, b, L.dout, out, ldo, gs);
+}
+
+__device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& L, int z, int64_t rows,
+                                          int row0, int nrows, float* out, float* red) {
+  const float* W = L.W + (size_t)z * L.wstride;
+  const float* b = L.b + (size_t)z * L.bstride;
+  const size_t so = ((size_t)z * rows + row0) * L.dout;
+  GSave gs{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
+  switch (L.act) {
+    case ACT_RELU: run_layer_act<ACT_RELU>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_SILU: run_layer_act<ACT_SILU>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_TANH: run_layer_act<ACT_TANH>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    default: run_layer_act<ACT_NONE>(in, LDH, L, W, b, out, LDH, red, gs); break;
+  }
+  (void)ldi;
+}
+
+// Runs net NI's layers (compile-time net and layer indices: runtime indexing into
+// the by-value kernarg struct would force a private-memory copy); returns the LDS
+// buffer holding the final activation.
+template <int NI>
+__device__ __forceinline__ float* run_net(const drpo_mlp_fwd_t& a, float* in, float* bufA, float* bufB, int z, int row0, int nrows,
+                          float* red) {
+  float* cur = in;
+#pragma unroll
+  for (int l = 0; l < MAXL; ++l) {
+    if (l < a.net[NI].nl) {
+      float* out = (cur == bufA) ? bufB : bufA;
+      run_layer(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red);
+      __syncthreads();
+      cur = out;
+    }
+  }
+  return cur;
+}
+
+__global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* xin = smem;                       // ROWS x LDH
+  float* bA = xin + FW_ROWS * LDH;
+  float* bB = bA + FW_ROWS * LDH;
+  float* T = bB + FW_ROWS * LDH;           // trunk output (trunk mode)
+  float* red = T + FW_ROWS * LDH;          // FW_NW * 256
+  const int tid = threadIdx.x;
+  const int z = blockIdx.z;
+  const int row0 = blockIdx.x * FW_ROWS;
+  if (row0 >= a.rows) return;
+  const int nrows = (int)min((int64_t)FW_ROWS, a.rows - row0);
+  const int din0 = a.cols[0] + a.cols[1] + a.cols[2];
+  const int kpad = round_up(din0, 16);
+
+  for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
+    const int r = e / kpad, k = e - r * kpad;
+    float v = 0.f;
+    if (r < nrows && k < din0) {
+      const int64_t row = row0 + r;
+      int kk = k;
+      const float* src;
+      if (kk < a.cols[0]) {
+        src = a.src[0] + (size_t)z * a.sstride[0] + row * a.ld[0];
+      } else if (kk - a.cols[0] < a.cols[1]) {
+        kk -= a.cols[0];
+        src = a.src[1] + (size_t)z * a.sstride[1] + row * a.ld[1];
+      } else {
+        kk -= a.cols[0] + a.cols[1];
+        src = a.src[2] + (size_t)z * a.sstride[2] + row * a.ld[2];
+      }
+      v = src[kk];
+      if (k < a.cols[0] && a.nmean) v = (v - a.nmean[kk]) / (a.nstd[kk] + 1e-6f);
+      if (a.save_x) a.save_x[((size_t)z * a.rows + row) * din0 + k] = v;
+    }
+    xin[r * LDH + k] = v;
+  }
+  __syncthreads();
+  if (!a.trunk) {
+    if (blockIdx.y == 0) run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
+    else if (blockIdx.y == 1) run_net<1>(a, xin, bA, bB, z, row0, nrows, red);
+    else run_net<2>(a, xin, bA, bB, z, row0, nrows, red);
+  } else {
+    float* t = run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
+    // move the trunk output out of the ping-pong pair
+    const int w = a.net[0].L[a.net[0].nl - 1].dout;
+    const int wpad = round_up(w, 16);
+    for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
+      const int r = e / wpad, k = e - r * wpad;
+      T[r * LDH + k] = t[r * LDH + k];
+    }
+    __syncthreads();
+    if (a.nnets > 1) run_net<1>(a, T, bA, bB, z, row0, nrows, red);
+    if (a.nnets > 2) run_net<2>(a, T, bA, bB, z, row0, nrows, red);
+  }
+}
+
+static size_t fwd_lds() { return sizeof(float) * ((size_t)4 * FW_ROWS * LDH + FW_NW * 256); }
+
+static int check_net(const drpo_mlp_net_t& n, int din) {
+  if (n.nl < 1 || n.nl > MAXL) return 0;
+  for (int l = 0; l < n.nl; ++l) {
+    if (n.L[l].din != din || n.L[l].dout < 1 || n.L[l].dout > 256 || !n.L[l].W) return 0;
+    din = n.L[l].dout;
+  }
+  return 1;
+}
+
+DRPO_API int drpo_mlp_forward(const drpo_mlp_fwd_t* a, hipStream_t stream) {
+  DRPO_REQUIRE(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_forward: bad descriptor");
+  const int din0 = a->cols[0] + a->cols[1] + a->cols[2];
+  DRPO_REQUIRE(din0 >= 1 && din0 <= 256, "drpo_mlp_forward: input width %d", din0);
+  if (a->trunk) {
+    DRPO_REQUIRE(check_net(a->net[0], din0), "drpo_mlp_forward: bad trunk");
+    const int tw = a->net[0].L[a->net[0].nl - 1].dout;
+    for (int h = 1; h < a->nnets; ++h) DRPO_REQUIRE(check_net(a->net[h], tw), "drpo_mlp_forward: bad head %d", h);
+  } else {
+    for (int h = 0; h < a->nnets; ++h) DRPO_REQUIRE(check_net(a->net[h], din0), "drpo_mlp_forward: bad net %d", h);
+  }
+  if (a->rows == 0) return DRPO_OK;
+  dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS), a->trunk ? 1 : a->nnets, a->nbatch);
+  mlp_fwd_kernel<<<grid, FW_NT, fwd_lds(), stream>>>(*a);
+  DRPO_LAUNCH_CHECK("mlp_forward");
+  return DRPO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// backward-data
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float act_grad(int act, float y, float z) {
+  switch (act) {
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_TANH: return 1.f - y * y;
+    case ACT_SILU: {
+      const float s = 1.f / (1.f + expf(-z));
+      return s * (1.f + z * (1.f - s));
+    }
+    default: return 1.f;
+  }
+}
+
+// G (LDS, width of the net output) -> gradient w.r.t. the net input (returned LDS buffer)
+__device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* G, float* bA, float* bB, int z, int64_t rows,
+                          int row0, int nrows) {
+  const int tid = threadIdx.x;
+  float* cur = G;
+  for (int l = net.nl - 1; l >= 0; --l) {
+    const drpo_mlp_bwd_layer_t& L = net.L[l];
+    const size_t so = ((size_t)z * rows + row0) * L.dout;
+    const int wpad = round_up(L.dout, 16);
+    for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
+      const int r = e / wpad, k = e - r * wpad;
+      float g = 0.f;
+      if (r < nrows && k < L.dout) {
+        g = cur[r * LDH + k];
+        if (L.act != ACT_NONE) {
+          const size_t idx = so + (size_t)r * L.dout + k;
+          g *= act_grad(L.act, L.sy ? L.sy[idx] : 0.f, L.sz ? L.sz[idx] : 0.f);
+        }
+        if (L.dz) L.dz[so + (size_t)r * L.dout + k] = g;
+      }
+      cur[r * LDH + k] = g;
+    }
+    __syncthreads();
+    float* out = (cur == bA) ? bB : bA;
+    const float* W = L.W + (size_t)z * L.wstride;
+    tile_dense_T<FW_NW, 1, FW_MAXC>(cur, LDH, L.dout, W, L.din, L.din, out, LDH);
+    __syncthreads();
+    cur = out;
+  }
+  return cur;
+}
+
+__global__ __launch_bounds__(FW_NT) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* G = smem;
+  float* bA = G + FW_ROWS * LDH;
+  float* bB = bA + FW_ROWS * LDH;
+  float* DT = bB + FW_ROWS * LDH;   // trunk output gradient accumulator
+  const int tid = threadIdx.x;
+  const int z = blockIdx.z;
+  const int row0 = blockIdx.x * FW_ROWS;
+  if (row0 >= a.rows) return;
+  const int nrows = (int)min((int64_t)FW_ROWS, a.rows - row0);
+
+  auto load_gout = [&](const drpo_mlp_bwd_net_t& n, float* dst) {
+    const int w = n.L[n.nl - 1].dout;
+    const int wpad = round_up(w, 16);
+    for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
+      const int r = e / wpad, k = e - r * wpad;
+      dst[r * LDH + k] = (r < nrows && k < w) ? n.gout[((size_t)z * a.rows + row0 + r) * w + k] : 0.f;
+    }
+    __syncthreads();
+  };
+  auto store_dx = [&](const drpo_mlp_bwd_net_t& n, const float* src) {
+    if (!n.dx) return;
+    for (int e = tid; e < nrows * n.dx_cols; e += FW_NT) {
+      const int r = e / n.dx_cols, k = e - r * n.dx_cols;
+      float* p = n.dx + ((size_t)z * a.rows + row0 + r) * n.dx_cols + k;
+      const float v = src[r * LDH + n.dx_col0 + k];
+      *p = n.dx_accumulate ? *p + v : v;
+    }
+  };
+
+  if (!a.trunk) {
+    const drpo_mlp_bwd_net_t& n = a.net[blockIdx.y];
+    load_gout(n, G);
+    const float* gx = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows);
+    store_dx(n, gx);
+    return;
+  }
+  const int tw = a.net[0].L[a.net[0].nl - 1].dout;
+  const int twpad = round_up(tw, 16);
+  for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) DT[(e / twpad) * LDH + e % twpad] = 0.f;
+  __syncthreads();
+  for (int h = 1; h < a.nnets; ++h) {
+    load_gout(a.net[h], G);
+    const float* gh = bwd_net(a.net[h], G, bA, bB, z, a.rows, row0, nrows);
+    for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) {
+      const int r = e / twpad, k = e - r * twpad;
+      DT[r * LDH + k] += gh[r * LDH + k];
+    }
+    __syncthreads();
+  }
+  const float* gx = bwd_net(a.net[0], DT, bA, bB, z, a.rows, row0, nrows);
+  store_dx(a.net[0], gx);
+}
+
+static size_t bwd_lds() { return sizeof(float) * (size_t)4 * FW_ROWS * LDH; }
+
+DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, hipStream_t stream) {
+  DRPO_REQUIRE(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_backward: bad descriptor");
+  for (int h = 0; h < a->nnets; ++h) {
+    const drpo_mlp_bwd_net_t& n = a->net[h];
+    DRPO_REQUIRE(n.nl >= 1 && n.nl <= MAXL && n.gout || (a->trunk && h == 0 && n.nl >= 1),
+                 "drpo_mlp_backward: bad net %d", h);
+    for (int l = 0; l < n.nl; ++l)
+      DRPO_REQUIRE(n.L[l].din >= 1 && n.L[l].din <= 256 && n.L[l].dout >= 1 && n.L[l].dout <= 256 && n.L[l].W,
+                   "drpo_mlp_backward: bad layer %d of net %d", l, h);
+    if (n.dx) DRPO_REQUIRE(n.dx_col0 >= 0 && n.dx_col0 + n.dx_cols <= n.L[0].din, "drpo_mlp_backward: dx columns");
+  }
+  if (a->rows == 0) return DRPO_OK;
+  dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS), a->trunk ? 1 : a->nnets, a->nbatch);
+  mlp_bwd_kernel<<<grid, FW_NT, bwd_lds(), stream>>>(*a);
+  DRPO_LAUNCH_CHECK("mlp_backward");
+  return DRPO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// grouped weight gradients
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int WG_TILE = 64;
+constexpr int WG_CHUNK = 1024;      // rows per workgroup (split-K over the batch)
+constexpr int WG_MAXITEMS = 16;
+constexpr int WG_LDK = 16 + 4;      // LDS [col][k] row stride
+}  // namespace
+
+struct WgradArgs {
+  drpo_wgrad_item_t it[WG_MAXITEMS];
+  int64_t first[WG_MAXITEMS + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[2][WG_TILE * WG_LDK];   // dz^T  [o][k]
+  __shared__ __attribute__((aligned(16))) float Bs[2][WG_TILE * WG_LDK];   // y^T   [i][k]
+  const int64_t bid = blockIdx.x;
+  int q = 0;
+  while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
+  const drpo_wgrad_item_t& I = a.it[q];
+  int64_t loc = bid - a.first[q];
+  const int ti = (I.din + 1 + WG_TILE - 1) / WG_TILE;      // +1: bias ("ones") column
+  const int to = (I.dout + WG_TILE - 1) / WG_TILE;
+  const int nch = (int)((I.rows + WG_CHUNK - 1) / WG_CHUNK);
+  const int ch = (int)(loc % nch); loc /= nch;
+  const int it_i = (int)(loc % ti); loc /= ti;
+  const int it_o = (int)(loc % to); loc /= to;
+  const int zb = (int)loc;
+  const float* dz = I.dz + (size_t)zb * I.zstride;
+  const float* y = I.y + (size_t)zb * I.ystride;
+  const int o0 = it_o * WG_TILE, i0 = it_i * WG_TILE;
+  const int64_t r0 = (int64_t)ch * WG_CHUNK;
+  const int64_t r1 = min(I.rows, r0 + WG_CHUNK);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  // staging: thread -> (k = tid >> 4, col4 = (tid & 15) * 4)
+  const int sk = tid >> 4, sc = (tid & 15) * 4;
+  float ra[4], rbv[4];
+  auto gload = [&](int64_t rbase) {
+    const int64_t r = rbase + sk;
+    const bool rok = r < r1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = o0 + sc + u, i = i0 + sc + u;
+      ra[u] = (rok && o < I.dout) ? dz[r * I.dout + o] : 0.f;
+      rbv[u] = (!rok || i > I.din) ? 0.f : (i == I.din ? 1.f : y[r * I.din + i]);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      As[buf][(sc + u) * WG_LDK + sk] = ra[u];
+      Bs[buf][(sc + u) * WG_LDK + sk] = rbv[u];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int w = 0; w < 2; ++w) acc[x][w] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ob = (wave >> 1) * 2, ib = (wave & 1) * 2;   // 16-blocks handled by this wave
+  gload(r0);
+  sstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t rb = r0; rb < r1; rb += 16) {
+    const bool more = rb + 16 < r1;
+    if (more) gload(rb + 16);
+    f32x4 fa[2], fb[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      fa[x] = *reinterpret_cast<const f32x4*>(&As[buf][((ob + x) * 16 + l15) * WG_LDK + 4 * g]);
+      fb[x] = *reinterpret_cast<const f32x4*>(&Bs[buf][((ib + x) * 16 + l15) * WG_LDK + 4 * g]);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int w = 0; w < 2; ++w)
+          acc[x][w] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x][m], fb[w][m], acc[x][w], 0, 0, 0);
+    if (more) {
+      sstore(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  float* gW = I.gW + (size_t)zb * I.gwstride;
+  float* gb = I.gb + (size_t)zb * I.gbstride;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const int i = i0 + (ib + w) * 16 + l15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + (ob + x) * 16 + 4 * g + r;
+        if (o >= I.dout || i > I.din) continue;
+        const float v = acc[x][w][r];
+        if (i < I.din) atomicAdd(&gW[(size_t)o * I.din + i], v);
+        else atomicAdd(&gb[o], v);
+      }
+    }
+}
+
+DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, hipStream_t stream) {
+  DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS, "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
+  WgradArgs a{};
+  int64_t tot = 0;
+  int m = 0;
+  for (int k = 0; k < n; ++k) {
+    const drpo_wgrad_item_t& I = items[k];
+    DRPO_REQUIRE(I.dz && I.y && I.gW && I.gb && I.dout >= 1 && I.din >= 1 && I.rows >= 0 && I.nbatch >= 1,
+                 "drpo_mlp_wgrad: bad item %d", k);
+    if (I.rows == 0) continue;
+    a.it[m] = I;
+    a.first[m] = tot;
+    const int64_t ti = (I.din + 1 + WG_TILE - 1) / WG_TILE, to = (I.dout + WG_TILE - 1) / WG_TILE;
+    tot += ti * to * ((I.rows + WG_CHUNK - 1) / WG_CHUNK) * I.nbatch;
+    ++m;
+  }
+  a.first[m] = tot;
+  a.n = m;
+  if (tot == 0) return DRPO_OK;
+  mlp_wgrad_kernel<<<(unsigned)tot, 256, 0, stream>>>(a);
+  DRPO_LAUNCH_CHECK("mlp_wgrad");
+  return DRPO_OK;
+}

@@ -1,0 +1,577 @@
+"""SAC engine: the safe-SAC update (src/ssac.py:437-578, src/smbpo.py:251-279) as a
+fixed sequence of HIP launches over engine-owned HBM workspaces.
+
+Per update_solver call (DRPO flags, actor on, multiplier on) the device runs:
+  sample_batch -> [critic] 8 fused MLP forwards/heads, critic_head (targets, losses,
+  output grads), 2 fused backward-data passes, 1 grouped weight-grad GEMM, clip +
+  Adam + EMA -> [actor] 7 forwards, upstream grads, 3 input-grad backwards, squash
+  backward, 1 backward + 1 weight-grad for both actors, clip + Adam (+ alpha) ->
+  [multiplier] 4 forwards, head, backward, weight-grad, clip + Adam.
+All launch descriptors point at static workspaces, so they are built once per
+batch size and the whole sequence is graph-capturable. Noise: Philox in the
+kernels (production) or the reference's recorded draws (parity TapeNoise), which
+are consumed here in the reference's call order.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._abi import (BufferView, CriticHead, MlpBwd, MlpFwd, WgradItem)
+from .optim import grad_sumsq, ema_
+
+ACT_ID = {None: 0, 'identity': 0, 'relu': 1, 'swish': 2, 'tanh': 3}
+
+# Philox call-site ids (production noise)
+SITE_PI_NEXT, SITE_SAFE_NEXT, SITE_PI_RS, SITE_SAFE_RS, SITE_PI_MULT = 1, 2, 5, 6, 8
+
+
+def spec_layers(group, prefix, spec, buf=None):
+    """[(W, b, din, dout, act)] for an MLPSpec stored under prefix in a flat group."""
+    out = []
+    n = spec.n_layers
+    for i in range(n):
+        act = spec.act if i < n - 1 else spec.out_act
+        W = group.view(f'{prefix}{2 * i}.weight', buf)
+        b = group.view(f'{prefix}{2 * i}.bias', buf)
+        out.append((W, b, spec.dims[i], spec.dims[i + 1], ACT_ID[act]))
+    return out
+
+
+class Net:
+    """One MLP as seen by the kernels: layer tuples + (optional) per-layer save buffers."""
+
+    def __init__(self, layers, grad_layers=None):
+        self.layers = layers              # [(W, b, din, dout, act)]
+        self.grad_layers = grad_layers    # [(gW, gb)] or None
+        self.sy = [None] * len(layers)
+        self.sz = [None] * len(layers)
+        self.dz = [None] * len(layers)
+
+    @property
+    def dout(self):
+        return self.layers[-1][3]
+
+    @property
+    def din(self):
+        return self.layers[0][2]
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, wstride=None, sstride=None):
+    d = MlpFwd()
+    for k, (t, cols) in enumerate(srcs):
+        d.src[k] = _p(t)
+        d.cols[k] = cols
+        d.ld[k] = t.shape[-1] if t is not None and t.dim() > 1 else 1
+        d.sstride[k] = 0 if sstride is None else sstride[k]
+    d.nmean, d.nstd = (norm[0].data_ptr(), norm[1].data_ptr()) if norm is not None else (0, 0)
+    d.save_x = _p(save_x)
+    for j, net in enumerate(nets):
+        d.net[j].nl = len(net.layers)
+        for l, (W, b, din, dout, act) in enumerate(net.layers):
+            L = d.net[j].L[l]
+            L.W, L.b, L.din, L.dout, L.act = W.data_ptr(), b.data_ptr(), din, dout, act
+            L.sy, L.sz = _p(net.sy[l]), _p(net.sz[l])
+            L.wstride, L.bstride = (0, 0) if wstride is None else wstride[j][l]
+    d.nnets, d.trunk, d.rows, d.nbatch = len(nets), int(trunk), rows, nbatch
+    return d
+
+
+def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None):
+    """nets[0] trunk when trunk=True (gouts[0] ignored); dx: {net_index: (tensor, col0, cols, accumulate)}."""
+    d = MlpBwd()
+    for j, net in enumerate(nets):
+        d.net[j].nl = len(net.layers)
+        for l, (W, b, din, dout, act) in enumerate(net.layers):
+            L = d.net[j].L[l]
+            L.W, L.din, L.dout, L.act = W.data_ptr(), din, dout, act
+            L.sy, L.sz, L.dz = _p(net.sy[l]), _p(net.sz[l]), _p(net.dz[l])
+            L.wstride = 0 if wstride is None else wstride[j][l][0]
+        d.net[j].gout = _p(gouts[j])
+        if dx and j in dx:
+            t, c0, nc, accum = dx[j]
+            d.net[j].dx, d.net[j].dx_col0, d.net[j].dx_cols, d.net[j].dx_accumulate = t.data_ptr(), c0, nc, int(accum)
+    d.nnets, d.trunk, d.rows, d.nbatch = len(nets), int(trunk), rows, nbatch
+    return d
+
+
+def wgrad_items(entries, rows):
+    """entries: [(net, inputs_per_layer)] -> ctypes array of WgradItem."""
+    items = []
+    for net, ins in entries:
+        for l, (W, b, din, dout, act) in enumerate(net.layers):
+            gW, gb = net.grad_layers[l]
+            it = WgradItem()
+            it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
+            it.dout, it.din, it.rows, it.nbatch = dout, din, rows, 1
+            items.append(it)
+    arr = (WgradItem * len(items))(*items)
+    return arr, len(items)
+
+
+class SACEngine:
+    def __init__(self, solver):
+        self.sol = solver
+        self.S, self.A, self.C = solver.state_dim, solver.action_dim, solver.con_dim
+        self.dev = solver.actor.group.data.device
+        self.B = None
+        self.ws = {}
+        self.loss_pool = None
+        self.loss_pos = 0
+        self.noise = None
+
+    # ------------------------------------------------------------------ buffers
+    def buf(self, name, *shape, dtype=torch.float32):
+        t = self.ws.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.zeros(*shape, dtype=dtype, device=self.dev)
+            self.ws[name] = t
+        return t
+
+    def _loss_slots(self, n):
+        if self.loss_pool is None or self.loss_pos + n > self.loss_pool.numel():
+            self.loss_pool = torch.zeros(1 << 16, device=self.dev)
+            self.loss_pos = 0
+        s = self.loss_pool[self.loss_pos:self.loss_pos + n]
+        self.loss_pos += n
+        return s
+
+    def _setup(self, B):
+        if self.B == B:
+            return
+        self.B = B
+        self.ws = {}
+        sol, S, A, C = self.sol, self.S, self.A, self.C
+        cg, tg = sol.critic_group, sol.critic_target_group
+        ag, sg, mg = sol.actor.group, sol.actor_safe.group, sol.multiplier.group
+        cspec, ccs = sol.critic.spec, sol.constraint_critic
+        buf = self.buf
+
+        def mk(group, prefix, spec, grads=True, data=None):
+            lay = spec_layers(group, prefix, spec, data)
+            gl = None
+            if grads:
+                gl = [(g[0], g[1]) for g in ((group.view(f'{prefix}{2 * i}.weight', group.grad),
+                                              group.view(f'{prefix}{2 * i}.bias', group.grad))
+                                             for i in range(spec.n_layers))]
+            return Net(lay, gl)
+
+        self.nets = n = {}
+        n['actor'] = mk(ag, 'net.', sol.actor.spec)
+        n['safe'] = mk(sg, 'net.', sol.actor_safe.spec)
+        n['q0'] = mk(cg, 'critic.qs.0.', cspec)
+        n['q1'] = mk(cg, 'critic.qs.1.', cspec)
+        n['q0t'] = mk(tg, 'critic.qs.0.', cspec, grads=False)
+        n['q1t'] = mk(tg, 'critic.qs.1.', cspec, grads=False)
+        for tag, grp, gr in (('', cg, True), ('t', tg, False)):
+            n['cc_trunk' + tag] = mk(grp, 'constraint_critic.trunk.', ccs.trunk_spec, gr)
+            n['cc_mean' + tag] = mk(grp, 'constraint_critic.mean_head.', ccs.mean_spec, gr)
+            n['cc_ls' + tag] = mk(grp, 'constraint_critic.log_std_head.', ccs.logstd_spec, gr)
+        n['mult'] = mk(mg, 'lam.', sol.multiplier.spec)
+        self.nets_view = {}
+        # forward saves (post-activations) and dz for every trained net
+        for key, net in n.items():
+            if net.grad_layers is None:
+                continue
+            for l, (_, _, din, dout, act) in enumerate(net.layers):
+                net.sy[l] = buf(f'{key}.sy{l}', B, dout)
+                net.dz[l] = buf(f'{key}.dz{l}', B, dout)
+        for key in ('q0t', 'q1t', 'cc_trunkt', 'cc_meant', 'cc_lst'):
+            net = n[key]
+            net.sy[-1] = buf(f'{key}.out', B, net.dout)
+        # batch
+        self.bs, self.ba, self.bs2 = buf('b.s', B, S), buf('b.a', B, A), buf('b.s2', B, S)
+        self.br, self.bh = buf('b.r', B), buf('b.h', B, C)
+        self.bd, self.bv = buf('b.d', B, dtype=torch.uint8), buf('b.v', B, dtype=torch.uint8)
+        # noise buffers (parity mode)
+        for k, shp in (('e1', (B, A)), ('e2', (B, A)), ('e3', (B, C)), ('e5', (B, A)), ('e6', (B, A)),
+                       ('e7', (B, A))):
+            buf(k, *shp)
+        buf('idx_r', B, dtype=torch.int64)
+        buf('idx_v', B, dtype=torch.int64)
+        self.desc = {}
+
+    # ------------------------------------------------------------------ noise
+    def _eps(self, name, arr):
+        if arr is None:
+            return None
+        t = self.ws[name]
+        t.view(-1)[:arr.size].copy_(torch.from_numpy(np.ascontiguousarray(arr, np.float32)).view(-1))
+        return t
+
+    # ------------------------------------------------------------------ helpers
+    def _run_fwd(self, key, builder):
+        d = self.desc.get(key)
+        if d is None:
+            d = self.desc[key] = builder()
+        _lib.check(_lib.lib().drpo_mlp_forward(ctypes.byref(d), _lib.stream()), key)
+
+    def _run_bwd(self, key, builder):
+        d = self.desc.get(key)
+        if d is None:
+            d = self.desc[key] = builder()
+        _lib.check(_lib.lib().drpo_mlp_backward(ctypes.byref(d), _lib.stream()), key)
+
+    def _run_wgrad(self, key, builder):
+        d = self.desc.get(key)
+        if d is None:
+            d = self.desc[key] = builder()
+        arr, n = d
+        _lib.check(_lib.lib().drpo_mlp_wgrad(arr, n, _lib.stream()), key)
+
+    def _policy_head(self, raw, mode, eps, site, ctr, a=None, logp=None, u=None, e=None, amean=None):
+        L = _lib.lib()
+        seed = self.noise.seed
+        _lib.check(L.drpo_policy_head(raw.data_ptr(), self.B, self.A, mode, _p(eps), seed, ctr, site, _p(a), _p(logp),
+                                      _p(u), _p(e), _p(amean), _lib.stream()), 'policy_head')
+
+    def _cc_head(self, mu, ls, ubmax, dist):
+        cc = self.sol.constraint_critic
+        _lib.check(_lib.lib().drpo_cc_head(mu.data_ptr(), ls.data_ptr(), self.B, self.C, int(dist), float(cc.std_ratio),
+                                           float(cc.log_std_min), float(cc.log_std_max), ubmax.data_ptr(), None,
+                                           _lib.stream()), 'cc_head')
+
+    def _clip_adam(self, opt, ranges, group, lr_scale=None):
+        """clip_grad_norm_ over each range separately (its own norm), then one Adam step
+        (shared step count / lr) over the ranges."""
+        sc = opt.step_scalars()
+        for (s0, s1) in ranges:
+            part = grad_sumsq(group.grad[s0:s1], self.buf(f'part.{group.name}.{s0}', 4096))
+            opt.apply(group.grad, s0, s1, sc, clip=(part, self.sol.grad_norm))
+
+    def _alive_span(self, group, prefixes):
+        spans = [group.span(p) for p in prefixes]
+        return min(s[0] for s in spans), max(s[1] for s in spans)
+
+    def _cc_nets(self, tag=''):
+        n = self.nets
+        return [n['cc_trunk' + tag], n['cc_mean' + tag], n['cc_ls' + tag]]
+
+    # ------------------------------------------------------------------ updates
+    def update_critic(self, obs, action, next_obs, reward, done, violation, constraint_value, noise=None):
+        """SSAC.update_critic (src/ssac.py:437-456). Returns (critic_loss, constraint_critic_loss) 0-d tensors."""
+        B = obs.shape[0]
+        self._setup(B)
+        for dst, src in ((self.bs, obs), (self.ba, action), (self.bs2, next_obs), (self.br, reward)):
+            dst.copy_(src.reshape(dst.shape))
+        self.bd.copy_(done.reshape(B).to(torch.uint8))
+        self.bv.copy_(violation.reshape(B).to(torch.uint8))
+        self.bh.copy_(constraint_value.reshape(B, self.C))
+        return self._critic_step(noise)
+
+    def _critic_step(self, noise):
+        sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        self.noise = noise = noise or self.noise
+        L = _lib.lib()
+        dist = sol.distributional_qc and sol.qc_under_uncertainty
+        if sol.qc_under_uncertainty and not sol.distributional_qc:
+            raise NotImplementedError('robust (model-sampled) certificate target: see DESIGN.md (next)')
+        qshape = (B,) if C == 1 else (B, C)
+        e1 = self._eps('e1', noise.normal((B, A)))
+        e2 = self._eps('e2', noise.normal((B, A)))
+        e3 = self._eps('e3', noise.randn_like(qshape)) if dist else None
+        noise.randn_like(qshape, used=False)       # loss forward's unused draw (src/ssac.py:80)
+        ctr = noise.next()
+        ws = self.ws
+        # target policy sample a' ~ pi(s'), log pi
+        self._run_fwd('c.actor', lambda: fill_fwd([self._out_net(n['actor'], 'c.raw_a', B)],
+                                                  [(self.bs2, S), (None, 0), (None, 0)], B))
+        self._policy_head(ws['c.raw_a'], 0, e1, SITE_PI_NEXT, ctr, a=self.buf('c.a2', B, A), logp=self.buf('c.lp2', B))
+        self._run_fwd('c.qt', lambda: fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (ws['c.a2'], A), (None, 0)], B))
+        # safe policy sample on s'
+        self._run_fwd('c.safe', lambda: fill_fwd([self._out_net(n['safe'], 'c.raw_s', B)],
+                                                 [(self.bs2, S), (None, 0), (None, 0)], B))
+        self._policy_head(ws['c.raw_s'], 0, e2, SITE_SAFE_NEXT, ctr, a=self.buf('c.a2s', B, A))
+        self._run_fwd('c.cct', lambda: fill_fwd(self._cc_nets('t'), [(self.bs2, S), (ws['c.a2s'], A), (None, 0)], B,
+                                                trunk=True))
+        # critics and constraint critic at (s, a) with saves
+        xs = self.buf('c.x', B, S + A)
+        self._run_fwd('c.q', lambda: fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B,
+                                              save_x=xs))
+        self._run_fwd('c.cc', lambda: fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B,
+                                               trunk=True))
+        loss = self._loss_slots(2)
+        sol.critic_group.grad.zero_()
+        ch = self.desc.get('c.head')
+        if ch is None:
+            ch = self.desc['c.head'] = CriticHead()
+            ch.B, ch.C = B, C
+            ch.r, ch.h, ch.d = self.br.data_ptr(), self.bh.data_ptr(), self.bd.data_ptr()
+            ch.q0t, ch.q1t, ch.logp2 = n['q0t'].sy[-1].data_ptr(), n['q1t'].sy[-1].data_ptr(), ws['c.lp2'].data_ptr()
+            ch.mu_t, ch.ls_t = n['cc_meant'].sy[-1].data_ptr(), n['cc_lst'].sy[-1].data_ptr()
+            ch.q0, ch.q1 = n['q0'].sy[-1].data_ptr(), n['q1'].sy[-1].data_ptr()
+            ch.mu, ch.ls = n['cc_mean'].sy[-1].data_ptr(), n['cc_ls'].sy[-1].data_ptr()
+            ch.dq0, ch.dq1 = self.buf('c.dq0', B).data_ptr(), self.buf('c.dq1', B).data_ptr()
+            ch.dmu, ch.dls = self.buf('c.dmu', B, C).data_ptr(), self.buf('c.dls', B, C).data_ptr()
+        cc = sol.constraint_critic
+        ch.distributional, ch.deterministic_backup = int(dist), int(sol.deterministic_backup)
+        ch.discount, ch.qc_td_bound = sol.discount, sol.qc_td_bound
+        ch.lmin, ch.lmax = cc.log_std_min, cc.log_std_max
+        ch.log_alpha = sol.log_alpha.data_ptr()
+        ch.eps3 = _p(e3)
+        ch.seed, ch.ctr = noise.seed, ctr
+        ch.loss = loss.data_ptr()
+        _lib.check(L.drpo_critic_head(ctypes.byref(ch), _lib.stream()), 'critic_head')
+        # backward: critics (twin) and constraint critic (trunk + heads)
+        self._run_bwd('c.bq', lambda: fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B))
+        heads = [n['cc_trunk'], n['cc_mean']] + ([n['cc_ls']] if dist else [])
+        self._run_bwd('c.bcc' + str(int(dist)), lambda: fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)],
+                                                                 B, trunk=True))
+        tsy = n['cc_trunk'].sy
+        items = [(n['q0'], [xs, n['q0'].sy[0], n['q0'].sy[1]]), (n['q1'], [xs, n['q1'].sy[0], n['q1'].sy[1]]),
+                 (n['cc_trunk'], [xs, tsy[0]]), (n['cc_mean'], [tsy[-1], n['cc_mean'].sy[0]])]
+        if dist:
+            items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]]))
+        self._run_wgrad('c.wg' + str(int(dist)), lambda: wgrad_items(items, B))
+        cg = sol.critic_group
+        crange = cg.span('critic.')
+        ccrange = self._alive_span(cg, ['constraint_critic.trunk.', 'constraint_critic.mean_head.'] +
+                                   (['constraint_critic.log_std_head.'] if dist else []))
+        sc = sol.critic_optimizer.step_scalars()
+        for (s0, s1) in (crange, ccrange):
+            part = grad_sumsq(cg.grad[s0:s1], self.buf(f'part.c.{s0}', 4096))
+            sol.critic_optimizer.apply(cg.grad, s0, s1, sc, clip=(part, sol.grad_norm))
+        sol.critic_lr_scheduler.step()
+        ema_(sol.critic_target_group.data, cg.data, sol.tau)
+        return loss[0], loss[1]
+
+    def _out_net(self, net, name, B):
+        """A no-save view of `net` whose final output lands in buffer `name`."""
+        v = Net(net.layers)
+        v.sy[-1] = self.buf(name, B, net.dout)
+        return v
+
+    # ------------------------------------------------------------------
+    def update_actor_and_alpha(self, obs, noise=None):
+        """SSAC.update_actor_and_alpha (src/ssac.py:458-527)."""
+        B = obs.shape[0]
+        self._setup(B)
+        self.bs.copy_(obs)
+        return self._actor_step(noise)
+
+    def _actor_step(self, noise):
+        sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        self.noise = noise = noise or self.noise
+        L = _lib.lib()
+        ws = self.ws
+        dist = sol.distributional_qc
+        qshape = (B,) if C == 1 else (B, C)
+        e5 = self._eps('e5', noise.std_normal((B, A)))
+        k = noise.choice(2)
+        if dist:
+            noise.randn_like(qshape, used=False)
+            noise.randn_like(qshape, used=False)
+        e6 = self._eps('e6', noise.std_normal((B, A)))
+        if dist:
+            noise.randn_like(qshape, used=False)
+        ctr = noise.next()
+        cc = sol.constraint_critic
+        # actor rsample with saves
+        xa = self.buf('a.x', B, S)
+        self._run_fwd('a.actor', lambda: fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa))
+        raw = n['actor'].sy[-1]
+        a, lp, u, e = self.buf('a.a', B, A), self.buf('a.lp', B), self.buf('a.u', B, A), self.buf('a.e', B, A)
+        self._policy_head(raw, 1, e5, SITE_PI_RS, ctr, a=a, logp=lp, u=u, e=e)
+        qk = n['q0'] if k == 0 else n['q1']
+        self._run_fwd(f'a.q{k}', lambda: fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B))
+        self._run_fwd('a.cc', lambda: fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B,
+                                               trunk=True))
+        # safe actor (rsample + its mean action)
+        xs = self.buf('a.xs', B, S)
+        self._run_fwd('a.safe', lambda: fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xs))
+        raws = n['safe'].sy[-1]
+        a_s, u_s, e_s, am = self.buf('a.as', B, A), self.buf('a.us', B, A), self.buf('a.es', B, A), \
+            self.buf('a.am', B, A)
+        self._policy_head(raws, 1, e6, SITE_SAFE_RS, ctr, a=a_s, u=u_s, e=e_s, amean=am)
+        # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad)
+        self._run_fwd('a.ccm', lambda: fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B,
+                                                trunk=True))
+        sqc = self.buf('a.sqc', B)
+        self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
+        self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
+                                                 [(self.bs, S), (sqc, 1), (None, 0)], B))
+        lams = self.buf('a.lams', B)
+        _lib.check(L.drpo_multiplier_out(B, ws['a.multx'].data_ptr(), float(sol.mlp_multiplier_cfg.upper_bound),
+                                         lams.data_ptr(), _lib.stream()), 'multiplier_out')
+        # constraint critic at (s, a_safe) with saves
+        self._run_fwd('a.cc2', lambda: fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B,
+                                                trunk=True))
+        # upstream gradients
+        ca, cs = self._cc_views('a.cc'), self._cc_views('a.cc2')
+        gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
+                                    self.buf('a.gmu2', B, C), self.buf('a.gls2', B, C))
+        _lib.check(L.drpo_actor_upstream(B, C, int(dist), float(cc.std_ratio), float(cc.log_std_min),
+                                         float(cc.log_std_max), lams.data_ptr(), ca[0].data_ptr(), ca[1].data_ptr(),
+                                         cs[0].data_ptr(), cs[1].data_ptr(), gq.data_ptr(), gmu.data_ptr(),
+                                         gls.data_ptr(), gmu2.data_ptr(), gls2.data_ptr(), _lib.stream()),
+                   'actor_upstream')
+        dA, dAs = self.buf('a.dA', B, A), self.buf('a.dAs', B, A)
+        self._run_bwd(f'a.bq{k}', lambda: fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)}))
+        hv = self.nets_view['a.cc']
+        self._run_bwd('a.bcc', lambda: fill_bwd(hv if dist else hv[:2], [None, gmu, gls][:3 if dist else 2], B,
+                                                trunk=True, dx={0: (dA, S, A, True)}))
+        hv2 = self.nets_view['a.cc2']
+        self._run_bwd('a.bcc2', lambda: fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B,
+                                                 trunk=True, dx={0: (dAs, S, A, False)}))
+        # squashed Gaussian backward -> actor heads; alpha loss sum
+        asum = self._loss_slots(1)
+        draw, draws = self.buf('a.draw', B, 2 * A), self.buf('a.draws', B, 2 * A)
+        _lib.check(L.drpo_squash_backward(B, A, raw.data_ptr(), u.data_ptr(), e.data_ptr(), dA.data_ptr(),
+                                          sol.log_alpha.data_ptr(), 1.0 / B, lp.data_ptr(),
+                                          float(sol.target_entropy), asum.data_ptr(), draw.data_ptr(),
+                                          _lib.stream()), 'squash_backward')
+        _lib.check(L.drpo_squash_backward(B, A, raws.data_ptr(), u_s.data_ptr(), e_s.data_ptr(), dAs.data_ptr(),
+                                          None, 0.0, None, 0.0, None, draws.data_ptr(), _lib.stream()),
+                   'squash_backward_safe')
+        sol.actor.group.grad.zero_()
+        sol.actor_safe.group.grad.zero_()
+        self._run_bwd('a.bact', lambda: fill_bwd([n['actor']], [draw], B))
+        self._run_bwd('a.bsafe', lambda: fill_bwd([n['safe']], [draws], B))
+        na, ns = n['actor'], n['safe']
+        self._run_wgrad('a.wg', lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]]), (ns, [xs, ns.sy[0], ns.sy[1]])],
+                                                    B))
+        # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam + cosine
+        g = sol.actor.group
+        self._clip_adam(sol.actor_optimizer, [(0, g.size)], g)
+        sol.actor_lr_scheduler.step()
+        ag = self.buf('a.alpha_grad', 1)
+        _lib.check(L.drpo_alpha_grad(sol.log_alpha.data_ptr(), asum.data_ptr(), B, ag.data_ptr(), _lib.stream()),
+                   'alpha_grad')
+        self._alpha_adam(ag)
+        g = sol.actor_safe.group
+        self._clip_adam(sol.actor_safe_optimizer, [(0, g.size)], g)
+        sol.actor_safe_lr_scheduler.step()
+
+    def _alpha_adam(self, grad):
+        opt = self.sol.alpha_optimizer
+        if opt.tensor is None:
+            opt.tensor = self.sol.log_alpha.view(1)
+        sc = opt.step_scalars()
+        opt.apply(grad, 0, 1, sc)
+
+    # views of nets with separately named save buffers (so passes do not clobber each other)
+    def _reuse(self, net, name):
+        v = self.nets_view.get(name)
+        if v is None:
+            v = Net(net.layers, net.grad_layers)
+            for l, (_, _, din, dout, act) in enumerate(net.layers):
+                v.sy[l] = self.buf(f'{name}.sy{l}', self.B, dout)
+            self.nets_view[name] = v
+        return v
+
+    def _reuse_cc(self, name):
+        v = self.nets_view.get(name)
+        if v is None:
+            v = [self._reuse(x, f'{name}.{i}') for i, x in enumerate(self._cc_nets())]
+            self.nets_view[name] = v
+        return v
+
+    def _cc_views(self, name):
+        v = self.nets_view[name]
+        return v[1].sy[-1], v[2].sy[-1]
+
+    def _outs_cc(self, name):
+        nets = [Net(x.layers) for x in self._cc_nets()]
+        nets[1].sy[-1] = self.buf(f'{name}.mu', self.B, self.C)
+        nets[2].sy[-1] = self.buf(f'{name}.ls', self.B, self.C)
+        return nets
+
+    # ------------------------------------------------------------------
+    def update_multiplier(self, obs, noise=None):
+        """SSAC.update_multiplier (src/ssac.py:529-578)."""
+        B = obs.shape[0]
+        self._setup(B)
+        self.bs.copy_(obs)
+        return self._mult_step(noise)
+
+    def _mult_step(self, noise):
+        sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        self.noise = noise = noise or self.noise
+        L = _lib.lib()
+        ws = self.ws
+        dist = sol.distributional_qc
+        qshape = (B,) if C == 1 else (B, C)
+        e7 = self._eps('e7', noise.std_normal((B, A)))
+        if dist:
+            noise.randn_like(qshape, used=False)
+            noise.randn_like(qshape, used=False)
+        ctr = noise.next()
+        self._run_fwd('m.actor', lambda: fill_fwd([self._out_net(n['actor'], 'm.raw', B)],
+                                                  [(self.bs, S), (None, 0), (None, 0)], B))
+        a = self.buf('m.a', B, A)
+        self._policy_head(ws['m.raw'], 1, e7, SITE_PI_MULT, ctr, a=a)
+        self._run_fwd('m.cc', lambda: fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B,
+                                               trunk=True))
+        aqc = self.buf('m.aqc', B)
+        self._cc_head(ws['m.cc.mu'], ws['m.cc.ls'], aqc, dist)
+        self._run_fwd('m.safe', lambda: fill_fwd([self._out_net(n['safe'], 'm.raws', B)],
+                                                 [(self.bs, S), (None, 0), (None, 0)], B))
+        am = self.buf('m.am', B, A)
+        self._policy_head(ws['m.raws'], 2, None, 0, ctr, amean=am)
+        self._run_fwd('m.ccs', lambda: fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B,
+                                                trunk=True))
+        sqc = self.buf('m.sqc', B)
+        self._cc_head(ws['m.ccs.mu'], ws['m.ccs.ls'], sqc, dist)
+        xm = self.buf('m.x', B, S + 1)
+        self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B, save_x=xm))
+        gx = self.buf('m.gx', B)
+        mc = sol.mlp_multiplier_cfg
+        _lib.check(L.drpo_multiplier_head(B, n['mult'].sy[-1].data_ptr(), sqc.data_ptr(), aqc.data_ptr(),
+                                          float(sol.constraint_threshold), float(sol.penalty_lb),
+                                          float(sol.penalty_ub), float(mc.upper_bound), float(sol.lam_epsilon),
+                                          gx.data_ptr(), None, _lib.stream()), 'multiplier_head')
+        g = sol.multiplier.group
+        g.grad.zero_()
+        nm = n['mult']
+        self._run_bwd('m.bmult', lambda: fill_bwd([nm], [gx], B))
+        self._run_wgrad('m.wg', lambda: wgrad_items([(nm, [xm, nm.sy[0], nm.sy[1]])], B))
+        self._clip_adam(sol.multiplier_optimizer, [(0, g.size)], g)
+        sol.multiplier_lr_scheduler.step()
+
+    # ------------------------------------------------------------------
+    def update_solver(self, alg, update_actor, update_multiplier, noise):
+        """SMBPO.update_solver (src/smbpo.py:251-279) from the device-resident buffers."""
+        sol = self.sol
+        B = sol.batch_size
+        self._setup(B)
+        self.noise = noise
+        n_real = int(alg.real_fraction * B)
+        rb, vb = alg.replay_buffer._module, alg.virt_buffer._module
+        ir = noise.randint(len(rb), n_real)
+        iv = noise.randint(None, B - n_real)
+        if ir is not None:
+            self.ws['idx_r'][:n_real].copy_(torch.from_numpy(ir))
+        if iv is not None:
+            self.ws['idx_v'][:B - n_real].copy_(torch.from_numpy(iv))
+        ctr = noise.next()
+
+        def view(b, dev_len):
+            v = BufferView()
+            v.s, v.a, v.s2, v.r = b._states.data_ptr(), b._actions.data_ptr(), b._next_states.data_ptr(), \
+                b._rewards.data_ptr()
+            v.h, v.d, v.v = b._constraint_values.data_ptr(), b._dones.data_ptr(), b._violations.data_ptr()
+            v.len = -1 if dev_len else len(b)
+            v.ptr_dev = b._pointer.data_ptr()
+            v.cap = b.capacity
+            return v
+
+        rv, vv = view(rb, False), view(vb, True)
+        L = _lib.lib()
+        _lib.check(L.drpo_sample_batch(ctypes.byref(rv), ctypes.byref(vv), n_real, B, self.S, self.A, self.C,
+                                       None if ir is None else self.ws['idx_r'].data_ptr(),
+                                       None if iv is None else self.ws['idx_v'].data_ptr(), noise.seed, ctr,
+                                       float(alg.reward_scale), float(alg.alive_bonus), float(alg.constraint_scale),
+                                       float(alg.constraint_offset), self.bs.data_ptr(), self.ba.data_ptr(),
+                                       self.bs2.data_ptr(), self.br.data_ptr(), self.bd.data_ptr(),
+                                       self.bv.data_ptr(), self.bh.data_ptr(), _lib.stream()), 'sample_batch')
+        lq, lqc = self._critic_step(noise)
+        if update_actor:
+            self._actor_step(noise)
+        if update_multiplier:
+            self._mult_step(noise)
+        return lq, lqc

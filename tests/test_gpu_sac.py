@@ -1,0 +1,102 @@
+"""HIP safe-SAC update parity against the reference's golden fixtures (recorded
+noise). Tolerances (fp32, after Adam steps): losses rtol 1e-4; parameters
+|d| <= 3e-5 + 1e-4*|ref| (one Adam step moves a weight by ~lr = 3e-4, so this
+catches any wrong gradient sign/magnitude while allowing fp32 summation-order
+differences); log_alpha likewise."""
+import numpy as np
+import pytest
+import torch
+
+import drpo_amd
+from conftest import load_golden
+from gpu_helpers import DEV, COMP, small_smbpo, load_sd, close
+
+pytestmark = pytest.mark.gpu
+PARAM_ATOL, PARAM_RTOL = 3e-5, 1e-4
+
+
+def solver_sd(d, prefix):
+    return {k[len(prefix):]: torch.from_numpy(np.array(d[k])) for k in d.files if k.startswith(prefix)}
+
+
+def check_params(module, ref, msg, skip=('model_ensemble', 'total_updates', 'log_alpha')):
+    sd = module.state_dict()
+    bad = []
+    for k, v in ref.items():
+        if k.startswith(skip):
+            continue
+        got = sd[k].detach().cpu().numpy()
+        exp = v.numpy()
+        err = np.abs(got - exp) - (PARAM_ATOL + PARAM_RTOL * np.abs(exp))
+        if (err > 0).any():
+            bad.append((k, float(np.abs(got - exp).max()), int((err > 0).sum()), exp.size))
+    assert not bad, f'{msg}: {bad[:6]}'
+
+
+@pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad'])
+def test_ssac_updates_match_reference(tag):
+    d = load_golden(f'ssac_{tag}')
+    env = str(d['meta/env'])
+    alg = small_smbpo(d, env)
+    sol = alg.solver
+    sd0 = solver_sd(d, 'sd0/')
+    sol.log_alpha.fill_(float(sd0.pop('log_alpha')))
+    missing, unexpected = sol.load_state_dict(sd0, strict=False)
+    assert not unexpected
+    batch = [torch.from_numpy(d['in/' + k]).to(DEV) for k in ['s', 'a', 's2', 'r', 'd', 'v', 'h']]
+    tape = drpo_amd.TapeNoise.from_npz(d, 'critic_tape')
+    lq, lqc = sol.update_critic(*batch, noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    np.testing.assert_allclose(lq.item(), float(d['out/lq']), rtol=1e-4)
+    np.testing.assert_allclose(lqc.item(), float(d['out/lqc']), rtol=1e-4)
+    check_params(sol, solver_sd(d, 'sd1/'), 'after update_critic')
+
+    tape = drpo_amd.TapeNoise.from_npz(d, 'actor_tape')
+    sol.update_actor_and_alpha(batch[0], noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    ref2 = solver_sd(d, 'sd2/')
+    np.testing.assert_allclose(sol.log_alpha.item(), float(ref2['log_alpha']), rtol=1e-5, atol=1e-6)
+    check_params(sol, ref2, 'after update_actor_and_alpha')
+
+    tape = drpo_amd.TapeNoise.from_npz(d, 'mult_tape')
+    sol.update_multiplier(batch[0], noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    check_params(sol, solver_sd(d, 'sd3/'), 'after update_multiplier')
+    lrs = [sol.critic_optimizer.lr, sol.actor_optimizer.lr, sol.actor_safe_optimizer.lr, sol.multiplier_optimizer.lr]
+    np.testing.assert_array_equal(np.array(lrs), d['lr3'])
+
+
+@pytest.mark.parametrize('env', ['point-robot', 'quadrotor'])
+def test_rollout_and_update_matches_reference(env):
+    """Two full SMBPO.rollout_and_update() calls (rollout + 10 update_solver each, the
+    reference cadence) from the post-fit state of the fixture."""
+    d = load_golden(f'smbpo_update_{env}')
+    alg = small_smbpo(d, env)
+    sd1 = {k[len('sd1/'):]: torch.from_numpy(np.array(d[k])) for k in d.files if k.startswith('sd1/')}
+    la = sd1.pop('log_alpha', None)
+    alg.load_state_dict(sd1, strict=False)
+    alg.solver.log_alpha.fill_(float(d['sd0/log_alpha']) if la is None else float(la))
+    rows = {k: torch.from_numpy(d['replay/' + k]).to(DEV) for k in COMP}
+    half = len(rows['states']) // 2
+    alg.replay_buffer.extend(**{k: v[:half] for k, v in rows.items()})
+    alg.replay_buffer.extend(**{k: v[half:] for k, v in rows.items()})
+    alg.model_ensemble._elite_inds = list(d['fit/elite_inds'])
+    for r in range(2):
+        tape = drpo_amd.TapeNoise.from_npz(d, f'rau{r}_tape')
+        alg.rollout_and_update(noise=tape)
+        torch.cuda.synchronize()
+        assert tape.done()
+    assert len(alg.virt_buffer) == int(d['virt/n'])
+    got = alg.virt_buffer.get(as_dict=True)
+    for k in COMP:
+        close(got[k], d['virt/' + k], tol=1e-3, msg=k)
+    ref = {k[len('sd2/'):]: torch.from_numpy(np.array(d[k])) for k in d.files if k.startswith('sd2/')}
+    np.testing.assert_allclose(alg.solver.log_alpha.item(), float(ref.pop('log_alpha')), rtol=1e-4, atol=1e-6)
+    check_params(alg, ref, 'after 2x rollout_and_update',
+                 skip=('model_ensemble', 'solver.model_ensemble', 'solver.total_updates', 'episodes', 'steps',
+                       'n_viol', 'epochs'))
+    lq = np.array([x.item() for x in alg.recent_critic_losses])
+    np.testing.assert_allclose(lq, d['losses/critic'], rtol=1e-3, atol=1e-5)
