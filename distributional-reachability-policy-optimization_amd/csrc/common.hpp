@@ -11,9 +11,9 @@
 #include <stdint.h>
 #include <string>
 
-#define DRPO_API extern "C" __attribute__((visibility("default")))
+#include "drpo_hip.h"
 
-enum DrpoStatus { DRPO_OK = 0, DRPO_EINVAL = 1, DRPO_EHIP = 2, DRPO_EUNSUPPORTED = 3 };
+#define DRPO_API extern "C" __attribute__((visibility("default")))
 
 void drpo_set_error(const char* fmt, ...);
 

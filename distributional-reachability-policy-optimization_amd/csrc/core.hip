@@ -32,7 +32,8 @@ DRPO_API int drpo_event_create(void** ev) {
 
 DRPO_API int drpo_event_destroy(void* ev) { return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? DRPO_OK : DRPO_EHIP; }
 
-DRPO_API int drpo_event_record(void* ev, hipStream_t stream) {
+DRPO_API int drpo_event_record(void* ev, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   return hipEventRecord((hipEvent_t)ev, stream) == hipSuccess ? DRPO_OK : DRPO_EHIP;
 }
 

@@ -29,72 +29,6 @@ constexpr int MAXN = 3;
 
 }  // namespace
 
-extern "C" {
-typedef struct {
-  const float* W;        // [dout][din] (member 0 when batched)
-  const float* b;        // [dout]
-  int din, dout, act;
-  float* sy;             // optional save of post-activation [rows][dout] (per batch item)
-  float* sz;             // optional save of pre-activation
-  int64_t wstride, bstride;   // batch (ensemble member) strides in floats
-} drpo_mlp_layer_t;
-
-typedef struct {
-  int nl;
-  drpo_mlp_layer_t L[3];
-} drpo_mlp_net_t;
-
-typedef struct {
-  const float* src[3];   // column-concatenated input sources
-  int cols[3];
-  int ld[3];
-  int64_t sstride[3];    // batch strides (floats)
-  const float* nmean;    // optional normalisation (x - mean) / (std + 1e-6) of src[0]
-  const float* nstd;
-  float* save_x;         // optional save of the assembled input [rows][din0]
-  drpo_mlp_net_t net[3];
-  int nnets;
-  int trunk;             // 1: net[0] is a trunk, net[1..] heads on its output
-  int64_t rows;          // rows per batch item
-  int nbatch;
-} drpo_mlp_fwd_t;
-
-typedef struct {
-  const float* W;
-  int din, dout, act;
-  const float* sy;       // saved post-activation (ReLU / tanh derivative)
-  const float* sz;       // saved pre-activation (SiLU derivative)
-  float* dz;             // optional save of dL/dZ [rows][dout] for weight grads
-  int64_t wstride;
-} drpo_mlp_bwd_layer_t;
-
-typedef struct {
-  int nl;
-  drpo_mlp_bwd_layer_t L[3];
-  const float* gout;     // dL/d(net output) [rows][dout_last]
-  float* dx;             // optional dL/d(net input) columns [dx_col0, dx_col0 + dx_cols) -> [rows][dx_cols]
-  int dx_col0, dx_cols, dx_accumulate;
-} drpo_mlp_bwd_net_t;
-
-typedef struct {
-  drpo_mlp_bwd_net_t net[3];
-  int nnets;
-  int trunk;             // 1: net[0] trunk; heads' input grads are summed into the trunk output grad
-  int64_t rows;
-  int nbatch;
-} drpo_mlp_bwd_t;
-
-typedef struct {
-  const float* dz;       // [rows][dout]
-  const float* y;        // layer input [rows][din]
-  float* gW;             // [dout][din] (+ member stride)
-  float* gb;             // [dout]
-  int dout, din;
-  int64_t rows;
-  int64_t zstride, ystride, gwstride, gbstride;   // batch strides
-  int nbatch;
-} drpo_wgrad_item_t;
-}
 
 // ---------------------------------------------------------------------------
 // forward
@@ -210,7 +144,8 @@ static int check_net(const drpo_mlp_net_t& n, int din) {
   return 1;
 }
 
-DRPO_API int drpo_mlp_forward(const drpo_mlp_fwd_t* a, hipStream_t stream) {
+DRPO_API int drpo_mlp_forward(const drpo_mlp_fwd_t* a, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_forward: bad descriptor");
   const int din0 = a->cols[0] + a->cols[1] + a->cols[2];
   DRPO_REQUIRE(din0 >= 1 && din0 <= 256, "drpo_mlp_forward: input width %d", din0);
@@ -332,7 +267,8 @@ __global__ __launch_bounds__(FW_NT) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
 
 static size_t bwd_lds() { return sizeof(float) * (size_t)4 * FW_ROWS * LDH; }
 
-DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, hipStream_t stream) {
+DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_backward: bad descriptor");
   for (int h = 0; h < a->nnets; ++h) {
     const drpo_mlp_bwd_net_t& n = a->net[h];
@@ -459,7 +395,8 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
     }
 }
 
-DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, hipStream_t stream) {
+DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS, "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
   WgradArgs a{};
   int64_t tot = 0;

@@ -33,7 +33,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 
 DRPO_API int drpo_grad_sumsq_blocks(int64_t n) { return (int)((n + SUMSQ_BLOCK_ELEMS - 1) / SUMSQ_BLOCK_ELEMS); }
 
-DRPO_API int drpo_grad_sumsq(const float* g, int64_t n, float* partial, hipStream_t stream) {
+DRPO_API int drpo_grad_sumsq(const float* g, int64_t n, float* partial, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(n >= 0, "drpo_grad_sumsq: n < 0");
   if (n == 0) return DRPO_OK;
   sumsq_kernel<<<drpo_grad_sumsq_blocks(n), 256, 0, stream>>>(g, n, partial);
@@ -92,7 +93,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 
 DRPO_API int drpo_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_over_bc1, float bc2_sqrt,
                        float beta1, float beta2, float eps, float weight_decay, const float* clip_partial,
-                       int n_partial, float max_norm, const float* lr_scale, hipStream_t stream) {
+                       int n_partial, float max_norm, const float* lr_scale, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(n >= 0 && p && g && m && v, "drpo_adam: bad arguments");
   if (n == 0) return DRPO_OK;
   AdamArgs a{p, g, m, v, n, lr_over_bc1, bc2_sqrt, beta1, beta2, 1.f - beta1, 1.f - beta2, eps, weight_decay,
@@ -109,7 +111,8 @@ __global__ void ema_kernel(float* t, const float* p, int64_t n, float rate, floa
     t[i] = rate * p[i] + keep * t[i];
 }
 
-DRPO_API int drpo_ema(float* target, const float* source, int64_t n, float rate, hipStream_t stream) {
+DRPO_API int drpo_ema(float* target, const float* source, int64_t n, float rate, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(rate >= 0.f && rate <= 1.f, "drpo_ema: rate must be in [0,1]");
   if (n == 0) return DRPO_OK;
   int blocks = (int)((n + 255) / 256);
@@ -176,7 +179,8 @@ DRPO_API size_t drpo_normalizer_workspace_size(int64_t N, int S) {
 }
 
 DRPO_API int drpo_normalizer_fit(const float* X, int64_t N, int S, float* mean, float* std, void* workspace,
-                                 hipStream_t stream) {
+                                 drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(N >= 1 && S >= 1 && S <= 256, "drpo_normalizer_fit: N=%lld S=%d", (long long)N, S);
   const int nb = (int)((N + NORM_ROWS - 1) / NORM_ROWS);
   colstats_partial_kernel<<<nb, 256, 2 * 256 * sizeof(double), stream>>>(X, N, S, (double*)workspace);
@@ -195,7 +199,8 @@ __global__ void normalize_kernel(const float* x, const float* mean, const float*
 }
 
 DRPO_API int drpo_normalize(const float* x, const float* mean, const float* std, float eps, float* y, int64_t n,
-                            int S, hipStream_t stream) {
+                            int S, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   if (n == 0) return DRPO_OK;
   int64_t blocks = (n * S + 255) / 256;
   if (blocks > 4096) blocks = 4096;

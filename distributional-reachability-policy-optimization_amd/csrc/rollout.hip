@@ -321,31 +321,6 @@ __global__ void rollout_finalize_kernel(int64_t* vptr, const int* n, int64_t* of
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-extern "C" {
-typedef struct {
-  int S, A, C, Ha, Hm, B, H;
-  int env_id, tracking_surr_start, tracking_n_surr;
-  float quad_x_threshold, quad_z_threshold;
-  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;
-  // ensemble parameters [E][out][in] / [E][out]
-  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2;
-  const float *norm_mean, *norm_std, *min_lv, *max_lv;
-  const int* members;              // host array [H]: elite member used at each step
-  const float* replay_states;
-  int64_t replay_ptr, replay_cap;
-  const int64_t* init_idx;         // device [B] chronological indices, or NULL (device PRP)
-  const float* eps_a;              // device [H][B][A] or NULL (Philox)
-  const float* eps_m;              // device [H][B][S+1] or NULL
-  uint64_t seed, ctr;
-  float *vs, *va, *vs2, *vr, *vh;
-  uint8_t *vd, *vv;
-  int64_t* vptr;                   // device: buffer pointer (advanced by the rollout)
-  int64_t vcap;
-  void* workspace;
-  int rows_per_tile;               // 16 or 32 (0: auto)
-  void** step_events;              // optional [2*H] hipEvent_t recorded around each step kernel
-} drpo_rollout_desc_t;
-}
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -405,7 +380,8 @@ static int hb_for(int64_t n) {
   return b;
 }
 
-DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, hipStream_t stream) {
+DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(d, "drpo_rollout: null descriptor");
   DRPO_REQUIRE(d->S >= 1 && d->S <= 64 && d->A >= 1 && d->A <= 8, "drpo_rollout: S=%d A=%d out of range", d->S, d->A);
   DRPO_REQUIRE(d->Ha >= 1 && d->Ha <= 256 && d->Hm >= 1 && d->Hm <= 256, "drpo_rollout: hidden dims must be <= 256");
@@ -501,7 +477,8 @@ __global__ void env_constraints_kernel(EnvParams ep, const float* s, int64_t n, 
 
 DRPO_API int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, float quad_x_threshold,
                                   float quad_z_threshold, const float* states, int64_t n, int S, uint8_t* done,
-                                  uint8_t* violation, float* h, hipStream_t stream) {
+                                  uint8_t* violation, float* h, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(env_id >= 0 && env_id <= 3, "drpo_env_constraints: unknown env id %d", env_id);
   if (n == 0) return DRPO_OK;
   EnvParams ep{env_id, tracking_surr_start, tracking_n_surr, quad_x_threshold, quad_z_threshold};
@@ -520,7 +497,8 @@ __global__ void prp_kernel(int64_t* out, int64_t B, int64_t N, int hb, uint32_t 
 }
 
 DRPO_API int drpo_sample_without_replacement(int64_t* out, int64_t B, int64_t N, uint64_t seed, uint64_t ctr,
-                                             hipStream_t stream) {
+                                             drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(B >= 0 && B <= N && N < (1ll << 62), "drpo_sample_without_replacement: need 0 <= B <= N");
   if (B == 0) return DRPO_OK;
   uint32_t k[4];

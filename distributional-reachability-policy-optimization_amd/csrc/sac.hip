@@ -62,15 +62,6 @@ __device__ __forceinline__ float cc_dstd_draw(float l, float lmin, float lmax, f
 // ---------------------------------------------------------------------------
 // minibatch sampling
 // ---------------------------------------------------------------------------
-extern "C" {
-typedef struct {
-  const float *s, *a, *s2, *r, *h;
-  const uint8_t *d, *v;
-  int64_t len;          // rows available (host-known), or -1: read min(*ptr_dev, cap)
-  const int64_t* ptr_dev;
-  int64_t cap;
-} drpo_buffer_view_t;
-}
 
 __global__ void sample_batch_kernel(drpo_buffer_view_t real, drpo_buffer_view_t virt, int n_real, int B, int S, int A,
                                     int C, const int64_t* idx_real, const int64_t* idx_virt, uint64_t seed,
@@ -117,7 +108,8 @@ DRPO_API int drpo_sample_batch(const drpo_buffer_view_t* real, const drpo_buffer
                                int S, int A, int C, const int64_t* idx_real, const int64_t* idx_virt, uint64_t seed,
                                uint64_t ctr, float reward_scale, float alive_bonus, float constraint_scale,
                                float constraint_offset, float* s, float* a, float* s2, float* r, uint8_t* d,
-                               uint8_t* v, float* h, hipStream_t stream) {
+                               uint8_t* v, float* h, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(real && virt && B >= 0 && n_real >= 0 && n_real <= B, "drpo_sample_batch: bad sizes");
   if (B == 0) return DRPO_OK;
   sample_batch_kernel<<<(B + 255) / 256, 256, 0, stream>>>(*real, *virt, n_real, B, S, A, C, idx_real, idx_virt, seed,
@@ -159,7 +151,8 @@ __global__ void policy_head_kernel(const float* raw, int64_t B, int A, int mode,
 
 DRPO_API int drpo_policy_head(const float* raw, int64_t B, int A, int mode, const float* eps, uint64_t seed,
                               uint64_t ctr, uint32_t site, float* a, float* logp, float* u, float* e, float* amean,
-                              hipStream_t stream) {
+                              drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(mode >= 0 && mode <= 2 && A >= 1, "drpo_policy_head: bad mode/A");
   if (B == 0) return DRPO_OK;
   policy_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(raw, B, A, mode, eps, seed, ctr, site, a, logp,
@@ -187,7 +180,8 @@ __global__ void cc_head_kernel(const float* mu, const float* lsraw, int64_t B, i
 }
 
 DRPO_API int drpo_cc_head(const float* mu, const float* lsraw, int64_t B, int C, int distributional, float std_ratio,
-                          float log_std_min, float log_std_max, float* ubmax, int* argmax, hipStream_t stream) {
+                          float log_std_min, float log_std_max, float* ubmax, int* argmax, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   cc_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(mu, lsraw, B, C, distributional, std_ratio,
                                                                   log_std_min, log_std_max, ubmax, argmax);
@@ -198,25 +192,6 @@ DRPO_API int drpo_cc_head(const float* mu, const float* lsraw, int64_t B, int C,
 // ---------------------------------------------------------------------------
 // critic + certificate targets, losses, gradients (update_critic)
 // ---------------------------------------------------------------------------
-extern "C" {
-typedef struct {
-  int64_t B;
-  int C;
-  int distributional, deterministic_backup;
-  float discount, qc_td_bound, lmin, lmax;
-  const float* log_alpha;                       // device scalar
-  const float *r, *h;                           // [B], [B][C] (preprocessed)
-  const uint8_t* d;                             // [B]
-  const float *q0t, *q1t, *logp2;               // target critics at (s', a'), log pi(a'|s')
-  const float *mu_t, *ls_t;                     // target constraint critic at (s', a'_safe) [B][C]
-  const float* eps3;                            // [B][C] sample noise (or NULL: Philox)
-  uint64_t seed, ctr;
-  const float *q0, *q1;                         // critics at (s, a)
-  const float *mu, *ls;                         // constraint critic at (s, a) [B][C]
-  float *dq0, *dq1, *dmu, *dls;                 // gradients (dls may be NULL in vanilla mode)
-  float* loss;                                  // [2]: critic loss, constraint-critic loss (accumulated)
-} drpo_critic_head_t;
-}
 
 __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) {
   __shared__ float red[8];
@@ -274,7 +249,8 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
   }
 }
 
-DRPO_API int drpo_critic_head(const drpo_critic_head_t* p, hipStream_t stream) {
+DRPO_API int drpo_critic_head(const drpo_critic_head_t* p, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(p && p->C >= 1 && p->B >= 0, "drpo_critic_head: bad descriptor");
   if (p->B == 0) return DRPO_OK;
   critic_head_kernel<<<(unsigned)((p->B + 255) / 256), 256, 0, stream>>>(*p);
@@ -329,7 +305,8 @@ __global__ void actor_upstream_kernel(int64_t B, int C, int dist, float ratio, f
 DRPO_API int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, float log_std_min,
                                  float log_std_max, const float* lams, const float* mu_a, const float* ls_a,
                                  const float* mu_s, const float* ls_s, float* gq, float* gmu_a, float* gls_a,
-                                 float* gmu_s, float* gls_s, hipStream_t stream) {
+                                 float* gmu_s, float* gls_s, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   actor_upstream_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(
       B, C, distributional, std_ratio, log_std_min, log_std_max, lams, mu_a, ls_a, mu_s, ls_s, gq, gmu_a, gls_a,
@@ -378,7 +355,8 @@ __global__ __launch_bounds__(256) void squash_bwd_kernel(int64_t B, int A, const
 
 DRPO_API int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, const float* e, const float* dA,
                                   const float* log_alpha, float lp_scale, const float* logp, float target_entropy,
-                                  float* alpha_sum, float* draw, hipStream_t stream) {
+                                  float* alpha_sum, float* draw, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   squash_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(B, A, raw, u, e, dA, log_alpha, lp_scale, logp,
                                                                      target_entropy, alpha_sum, draw);
@@ -391,7 +369,8 @@ __global__ void alpha_grad_kernel(const float* log_alpha, const float* alpha_sum
 }
 
 DRPO_API int drpo_alpha_grad(const float* log_alpha, const float* alpha_sum, int64_t B, float* grad,
-                             hipStream_t stream) {
+                             drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   alpha_grad_kernel<<<1, 1, 0, stream>>>(log_alpha, alpha_sum, 1.f / (float)B, grad);
   DRPO_LAUNCH_CHECK("alpha_grad");
   return DRPO_OK;
@@ -427,7 +406,8 @@ __global__ __launch_bounds__(256) void multiplier_head_kernel(int64_t B, const f
 
 DRPO_API int drpo_multiplier_head(int64_t B, const float* x, const float* safe_qc, const float* actor_qc,
                                   float threshold, float penalty_lb, float penalty_ub, float upper_bound,
-                                  float lam_epsilon, float* gx, float* loss, hipStream_t stream) {
+                                  float lam_epsilon, float* gx, float* loss, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   multiplier_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(
       B, x, safe_qc, actor_qc, threshold, penalty_lb, penalty_ub, upper_bound, lam_epsilon, gx, loss);
@@ -441,7 +421,8 @@ __global__ void multiplier_out_kernel(int64_t B, const float* x, float ub, float
   if (i < B) lam[i] = ub / 2.f * (1.f + tanhf(x[i] / ub * 2.f));
 }
 
-DRPO_API int drpo_multiplier_out(int64_t B, const float* x, float upper_bound, float* lam, hipStream_t stream) {
+DRPO_API int drpo_multiplier_out(int64_t B, const float* x, float upper_bound, float* lam, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   multiplier_out_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(B, x, upper_bound, lam);
   DRPO_LAUNCH_CHECK("multiplier_out");

@@ -1,0 +1,256 @@
+/*
+ * drpo_hip.h -- C ABI of libdrpo_hip.so, the MI355X (gfx950) hot path of
+ * Distributional Reachability Policy Optimization.
+ *
+ * The reference (ManUtdMoon/Distributional-Reachability-Policy-Optimization) is
+ * pure Python/PyTorch with no FFI; these entry points are what a binding for its
+ * hot path binds (the Python package drpo_amd binds them with ctypes, see
+ * INTEGRATION.md). Conventions:
+ *   - all pointers are DEVICE pointers (fp32 row-major, uint8 flags, int64
+ *     indices) unless marked "host"; memory is owned by the caller (PyTorch's
+ *     caching allocator), the library never allocates on the hot path;
+ *   - every call is asynchronous on `stream` (a hipStream_t passed as void*);
+ *   - return 0 on success, DRPO_EINVAL / DRPO_EHIP / DRPO_EUNSUPPORTED
+ *     otherwise, with a message in drpo_last_error() (thread-local);
+ *   - noise: a non-NULL eps pointer is "parity mode" (the caller supplies the
+ *     reference's standard-normal draws); NULL means Philox4x32-10 on the device
+ *     keyed by (seed, ctr, call-site).
+ * Reference citations are path:line in the reference repository.
+ */
+#ifndef DRPO_HIP_H
+#define DRPO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* drpo_stream_t; /* hipStream_t */
+
+enum { DRPO_OK = 0, DRPO_EINVAL = 1, DRPO_EHIP = 2, DRPO_EUNSUPPORTED = 3 };
+
+/* activation ids used by the MLP descriptors (src/torch_util.py:169-178) */
+enum { DRPO_ACT_NONE = 0, DRPO_ACT_RELU = 1, DRPO_ACT_SILU = 2, DRPO_ACT_TANH = 3 };
+
+/* device environment ids for the batched constraint functions (src/smbpo.py:63-65) */
+enum { DRPO_ENV_POINT_ROBOT = 0, DRPO_ENV_QUADROTOR = 1, DRPO_ENV_CARTPOLE = 2, DRPO_ENV_TRACKING = 3 };
+
+/* ---------------------------------------------------------------- library */
+int drpo_version(void);
+const char* drpo_last_error(void);
+int drpo_event_create(void** ev);
+int drpo_event_destroy(void* ev);
+int drpo_event_record(void* ev, drpo_stream_t stream);
+int drpo_event_elapsed_ms(float* ms /* host */, void* start, void* stop);
+
+/* ---------------------------------------------------------------- rollout
+ * Replaces SMBPO.rollout (src/smbpo.py:229-249) together with
+ * BatchedGaussianEnsemble.sample (src/dynamics.py:198-203, _forward1 :112-122),
+ * SquashedGaussianPolicy.act(eval=False) (src/policy.py:77-97), the env
+ * check_done / check_violation / get_constraint_values round trips
+ * (src/smbpo.py:63-65) and ConstraintSafetySampleBuffer.extend into the virtual
+ * buffer (src/sampling.py:128-145): one fused kernel per horizon step, rows that
+ * are done are compacted away (order preserving) on the device.            */
+typedef struct {
+  int S, A, C, Ha, Hm, B, H;
+  int env_id, tracking_surr_start, tracking_n_surr;
+  float quad_x_threshold, quad_z_threshold;
+  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;          /* actor Linear layers [out][in] */
+  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2; /* ensemble [E][out][in] */
+  const float *norm_mean, *norm_std, *min_lv, *max_lv;
+  const int* members;            /* host [H]: elite member per step (random.choice, src/dynamics.py:199) */
+  const float* replay_states;    /* real buffer states, physical layout */
+  int64_t replay_ptr, replay_cap;
+  const int64_t* init_idx;       /* [B] chronological indices (np.random.choice) or NULL: device sampling w/o replacement */
+  const float* eps_a;            /* [H][B][A] or NULL */
+  const float* eps_m;            /* [H][B][S+1] or NULL */
+  uint64_t seed, ctr;
+  float *vs, *va, *vs2, *vr, *vh;  /* virtual buffer components */
+  uint8_t *vd, *vv;
+  int64_t* vptr;                 /* device int64 write pointer, advanced by the rollout */
+  int64_t vcap;
+  void* workspace;               /* drpo_rollout_workspace_size bytes */
+  int rows_per_tile;             /* 16 or 32, 0 = auto */
+  void** step_events;            /* optional [2*H] events recorded around each step kernel */
+} drpo_rollout_desc_t;
+
+size_t drpo_rollout_workspace_size(int B, int S, int H);
+size_t drpo_rollout_count_offset(int B, int S, int H); /* byte offset of the int64 row count in the workspace */
+int drpo_rollout(const drpo_rollout_desc_t* d /* host */, drpo_stream_t stream);
+
+/* batched env constraint functions, e.g. PointRobot.get_constraint_values /
+ * check_violation / check_done (src/env/point_robot.py:96-131); h is [n][C] */
+int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, float quad_x_threshold,
+                         float quad_z_threshold, const float* states, int64_t n, int S, uint8_t* done,
+                         uint8_t* violation, float* h, drpo_stream_t stream);
+
+/* B distinct indices in [0, N): production stand-in for random_choice(replace=False)
+ * (src/torch_util.py:41-48) */
+int drpo_sample_without_replacement(int64_t* out, int64_t B, int64_t N, uint64_t seed, uint64_t ctr,
+                                    drpo_stream_t stream);
+
+/* ---------------------------------------------------------------- MLPs
+ * Fused forward / backward-data / weight-gradient passes for mlp() nets
+ * (src/torch_util.py:190-211) and BatchedLinear ensembles (src/dynamics.py:26-52,
+ * nbatch = ensemble members). Used by the SAC update (src/ssac.py:437-578),
+ * the ensemble fit (src/dynamics.py:143-187) and every network forward.      */
+typedef struct {
+  const float* W; /* [dout][din] */
+  const float* b; /* [dout] */
+  int din, dout, act;
+  float* sy;      /* optional: post-activation save [rows][dout] */
+  float* sz;      /* optional: pre-activation save */
+  int64_t wstride, bstride; /* per batch item (ensemble member) */
+} drpo_mlp_layer_t;
+
+typedef struct {
+  int nl;
+  drpo_mlp_layer_t L[3];
+} drpo_mlp_net_t;
+
+typedef struct {
+  const float* src[3]; /* column-concatenated input sources (e.g. torch.cat([s, a], -1)) */
+  int cols[3];
+  int ld[3];
+  int64_t sstride[3];
+  const float* nmean;  /* optional (src[0] - mean) / (std + 1e-6) (src/normalization.py:22-23) */
+  const float* nstd;
+  float* save_x;       /* optional save of the assembled input */
+  drpo_mlp_net_t net[3];
+  int nnets;
+  int trunk;           /* 1: net[0] trunk, net[1..] heads on its output */
+  int64_t rows;
+  int nbatch;
+} drpo_mlp_fwd_t;
+
+typedef struct {
+  const float* W;
+  int din, dout, act;
+  const float* sy;
+  const float* sz;
+  float* dz;           /* optional save of dL/dZ for weight gradients */
+  int64_t wstride;
+} drpo_mlp_bwd_layer_t;
+
+typedef struct {
+  int nl;
+  drpo_mlp_bwd_layer_t L[3];
+  const float* gout;   /* dL/d(output) [rows][dout_last] */
+  float* dx;           /* optional dL/d(input) for input columns [dx_col0, dx_col0 + dx_cols) */
+  int dx_col0, dx_cols, dx_accumulate;
+} drpo_mlp_bwd_net_t;
+
+typedef struct {
+  drpo_mlp_bwd_net_t net[3];
+  int nnets;
+  int trunk;
+  int64_t rows;
+  int nbatch;
+} drpo_mlp_bwd_t;
+
+typedef struct {
+  const float* dz; /* [rows][dout] */
+  const float* y;  /* layer input [rows][din] */
+  float* gW;       /* accumulated into (atomics): caller zeroes before the backward pass */
+  float* gb;
+  int dout, din;
+  int64_t rows;
+  int64_t zstride, ystride, gwstride, gbstride;
+  int nbatch;
+} drpo_wgrad_item_t;
+
+int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);
+int drpo_mlp_backward(const drpo_mlp_bwd_t* desc /* host */, drpo_stream_t stream);
+int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, drpo_stream_t stream);
+
+/* ---------------------------------------------------------------- SAC heads
+ * (src/ssac.py:284-578, src/smbpo.py:251-279, src/policy.py:89-97)            */
+typedef struct {
+  const float *s, *a, *s2, *r, *h;
+  const uint8_t *d, *v;
+  int64_t len;          /* rows available, or -1: min(*ptr_dev, cap) read on the device */
+  const int64_t* ptr_dev;
+  int64_t cap;
+} drpo_buffer_view_t;
+
+/* mixed real/virtual minibatch (src/smbpo.py:253-270; SampleBuffer.sample src/sampling.py:147-151) */
+int drpo_sample_batch(const drpo_buffer_view_t* real, const drpo_buffer_view_t* virt, int n_real, int B, int S, int A,
+                      int C, const int64_t* idx_real, const int64_t* idx_virt, uint64_t seed, uint64_t ctr,
+                      float reward_scale, float alive_bonus, float constraint_scale, float constraint_offset, float* s,
+                      float* a, float* s2, float* r, uint8_t* d, uint8_t* v, float* h, drpo_stream_t stream);
+
+/* squashed Gaussian (src/policy.py:89-97, src/squashed_gaussian.py): mode 0 sample,
+ * 1 rsample, 2 mean (tanh(mu)); raw = [mu | log-std pre-activation] [B][2A] */
+int drpo_policy_head(const float* raw, int64_t B, int A, int mode, const float* eps, uint64_t seed, uint64_t ctr,
+                     uint32_t site, float* a, float* logp, float* u, float* e, float* amean, drpo_stream_t stream);
+
+/* ConstraintCritic log-std clamp + quantile bound mu + std_ratio*std, max over C
+ * (src/ssac.py:64-92, _get_qc :588-600) */
+int drpo_cc_head(const float* mu, const float* lsraw, int64_t B, int C, int distributional, float std_ratio,
+                 float log_std_min, float log_std_max, float* ubmax, int* argmax, drpo_stream_t stream);
+
+typedef struct {
+  int64_t B;
+  int C;
+  int distributional, deterministic_backup;
+  float discount, qc_td_bound, lmin, lmax;
+  const float* log_alpha;
+  const float *r, *h;
+  const uint8_t* d;
+  const float *q0t, *q1t, *logp2;
+  const float *mu_t, *ls_t;
+  const float* eps3;
+  uint64_t seed, ctr;
+  const float *q0, *q1;
+  const float *mu, *ls;
+  float *dq0, *dq1, *dmu, *dls;
+  float* loss; /* [2] accumulated: critic loss, constraint-critic loss */
+} drpo_critic_head_t;
+
+/* compute_target + compute_cons_target + critic / constraint-critic losses and
+ * their output gradients (src/ssac.py:284-435) */
+int drpo_critic_head(const drpo_critic_head_t* p /* host */, drpo_stream_t stream);
+
+/* dL/d outputs of the critic and constraint critic for actor_loss (src/ssac.py:458-505) */
+int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, float log_std_min, float log_std_max,
+                        const float* lams, const float* mu_a, const float* ls_a, const float* mu_s, const float* ls_s,
+                        float* gq, float* gmu_a, float* gls_a, float* gmu_s, float* gls_s, drpo_stream_t stream);
+
+/* chain rule through rsample/tanh/log_prob to the actor head; alpha-loss sum */
+int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, const float* e, const float* dA,
+                         const float* log_alpha, float lp_scale, const float* logp, float target_entropy,
+                         float* alpha_sum, float* draw, drpo_stream_t stream);
+
+/* d alpha_loss / d log_alpha (src/ssac.py:498-501) */
+int drpo_alpha_grad(const float* log_alpha, const float* alpha_sum, int64_t B, float* grad, drpo_stream_t stream);
+
+/* multiplier loss gradient w.r.t. the MLPMultiplier output (src/ssac.py:529-568) */
+int drpo_multiplier_head(int64_t B, const float* x, const float* safe_qc, const float* actor_qc, float threshold,
+                         float penalty_lb, float penalty_ub, float upper_bound, float lam_epsilon, float* gx,
+                         float* loss, drpo_stream_t stream);
+/* MLPMultiplier.forward output transform (src/ssac.py:107-111) */
+int drpo_multiplier_out(int64_t B, const float* x, float upper_bound, float* lam, drpo_stream_t stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * torch.optim.Adam (coupled L2), clip_grad_norm_, update_ema (src/ssac.py:446-455,
+ * src/torch_util.py:223-226), over flat parameter groups                       */
+int drpo_grad_sumsq_blocks(int64_t n);
+int drpo_grad_sumsq(const float* g, int64_t n, float* partial, drpo_stream_t stream);
+int drpo_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_over_bc1, float bc2_sqrt, float beta1,
+              float beta2, float eps, float weight_decay, const float* clip_partial, int n_partial, float max_norm,
+              const float* lr_scale, drpo_stream_t stream);
+int drpo_ema(float* target, const float* source, int64_t n, float rate, drpo_stream_t stream);
+
+/* Normalizer.fit / forward (src/normalization.py:14-23) */
+size_t drpo_normalizer_workspace_size(int64_t N, int S);
+int drpo_normalizer_fit(const float* X, int64_t N, int S, float* mean, float* std, void* workspace,
+                        drpo_stream_t stream);
+int drpo_normalize(const float* x, const float* mean, const float* std, float eps, float* y, int64_t n, int S,
+                   drpo_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRPO_HIP_H */
