@@ -25,6 +25,15 @@ void drpo_set_error(const char* fmt, ...);
     }                                       \
   } while (0)
 
+#define DRPO_CHECK_HIP(expr)                                                  \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      drpo_set_error("%s failed: %s", #expr, hipGetErrorString(_e));          \
+      return DRPO_EHIP;                                                       \
+    }                                                                         \
+  } while (0)
+
 #define DRPO_LAUNCH_CHECK(name)                                               \
   do {                                                                        \
     hipError_t _e = hipGetLastError();                                        \

@@ -103,14 +103,21 @@ class BatchedGaussianEnsemble(Configurable, Module):
         return (layer_views(g, 'trunk.', self.trunk_spec, buf), layer_views(g, 'diff_head.', self.diff_spec, buf),
                 layer_views(g, 'log_var_head.', self.logvar_spec, buf))
 
-    # API (compute in ops.py) ----------------------------------------------
+    # API (compute in ensemble_engine.py) ------------------------------------
+    @property
+    def engine(self):
+        eng = self.__dict__.get('_engine')
+        if eng is None:
+            from .ensemble_engine import EnsembleEngine
+            eng = EnsembleEngine(self)
+            self.__dict__['_engine'] = eng
+        return eng
+
     def _forward1(self, states, actions, index):
-        from . import ops
-        return ops.ensemble_forward1(self, states, actions, index)
+        return self.engine.forward1(states, actions, index)
 
     def _forward_all(self, states, actions):
-        from . import ops
-        return ops.ensemble_forward_all(self, states, actions)
+        return self.engine.forward_all(states, actions)
 
     def _rebatch(self, x):
         n = len(x)
@@ -119,30 +126,44 @@ class BatchedGaussianEnsemble(Configurable, Module):
 
     def sample(self, states, actions, noise=None):
         import random
-        from . import ops
         index = self._elite_inds[random.choice(range(len(self._elite_inds))) if noise is None
                                  else noise.choice(len(self._elite_inds))]
-        return ops.ensemble_sample(self, states, actions, index, noise)
+        return self.engine.sample(states, actions, index, noise)
 
     def means(self, states, actions):
-        states = states.repeat(self.ensemble_size, 1, 1)
-        actions = actions.repeat(self.ensemble_size, 1, 1)
-        means, _ = self._forward_all(states, actions)
+        # states.repeat(E, 1, 1) of the reference == member stride 0 (no copy)
+        means, _ = self._forward_all(states.unsqueeze(0), actions.unsqueeze(0))
         return means[:, :, :-1], means[:, :, -1]
 
     def mean(self, states, actions):
         s, r = self.means(states, actions)
         return s.mean(dim=0), r.mean(dim=0)
 
+    def elite_samples(self, states, actions, noise=None):
+        return self.engine.elite_samples(states, actions, list(self._elite_inds), noise)
+
     def compute_loss(self, states, actions, targets):
-        from . import ops
-        return ops.ensemble_compute_loss(self, states, actions, targets)
+        from .ensemble_engine import EnsembleLoss
+        anchor = self.__dict__.get('_anchor')
+        if anchor is None:
+            anchor = self.__dict__['_anchor'] = torch.zeros((), requires_grad=True)
+        if torch.is_grad_enabled():
+            return EnsembleLoss.apply(anchor, self.engine, states, actions, targets)
+        return self.engine.compute_loss_value(states, actions, targets)
+
+    def _mse_loss(self, states, actions, targets, enable_grad=True):
+        """Per-member NLL [E] (values only; gradients flow through compute_loss)."""
+        e = self.engine
+        s, a, t = e._prep(states, actions, targets)
+        E, b, S = s.shape
+        nets, _, _ = e._forward(s, a, b, E, b * S, b * self.action_dim, tag='mse')
+        mse, _, _ = e._loss(nets, s, b * S, t, b * (S + 1), b, E, False, tag='mse')
+        return mse.clone()
 
     def fit(self, buffer, steps=None, epochs=None, progress_bar=False, noise=None, **kwargs):
-        from . import ops
         if steps is not None:
             assert epochs is None, 'Cannot pass both steps and epochs'
-            return ops.ensemble_fit(self, buffer, steps, noise)
+            return self.engine.fit(buffer, steps, noise)
         if epochs is not None:
-            raise NotImplementedError('epochal fit: use src/train.py epochal_training with compute_loss/optimizer')
+            return self.engine.fit_epochs(buffer, epochs, **kwargs)
         raise ValueError('Must pass steps or epochs')

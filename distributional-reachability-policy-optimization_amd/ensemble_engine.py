@@ -1,0 +1,337 @@
+"""Dynamics-ensemble engine: BatchedGaussianEnsemble's forward / sample / loss / fit
+(src/dynamics.py:112-253) as HIP launches over the model's flat HBM group.
+
+Every pass is one fused MLP launch over all members (grid.z = member; weights are
+the [E, out, in] BatchedLinear layout, so member z reads W + z*out*in) around
+small row-wise kernels (csrc/ensemble.hip):
+
+  forward     drpo_mlp_forward (trunk + diff head + log-var head in one launch)
+              -> drpo_ens_head (residual mean, soft log-var clamp [, sample])
+  fit step    drpo_ens_gather -> forward (saving activations) -> drpo_ens_loss
+              (NLL + bound term + output grads) -> drpo_mlp_backward (heads into
+              the shared trunk) -> drpo_mlp_wgrad (all 6 layers x E members, one
+              launch) -> drpo_adam over the whole group
+  holdout     gather -> forward with member stride 0 (the reference's
+              .repeat(E, 1) without the copy) -> drpo_ens_loss (no grads)
+
+The per-step ``loss.item()`` of the reference is deferred: losses land in a device
+array that is read once at the end of fit (same returned list of floats).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .rng import DeviceNoise
+from .sac_step import ACT_ID, Net, fill_bwd, fill_fwd
+from ._abi import WgradItem
+
+
+class EnsembleEngine:
+    def __init__(self, model):
+        self.m = model
+        self.ws = {}
+        self.noise = None
+        self.dev = model.group.data.device
+
+    # ------------------------------------------------------------------ helpers
+    def buf(self, name, *shape, dtype=torch.float32):
+        t = self.ws.get(name)
+        if t is None or t.numel() < int(np.prod(shape)) or t.dtype != dtype:
+            t = torch.empty(int(np.prod(shape)), dtype=dtype, device=self.dev)
+            self.ws[name] = t
+        return t[:int(np.prod(shape))].view(*shape)
+
+    def _noise(self, noise):
+        if noise is not None:
+            return noise
+        if self.noise is None:
+            self.noise = DeviceNoise(torch.initial_seed() ^ 0x5EED0DE1)
+        return self.noise
+
+    def _specs(self):
+        m = self.m
+        return (('trunk.', m.trunk_spec), ('diff_head.', m.diff_spec), ('log_var_head.', m.logvar_spec))
+
+    def _nets(self, member=None, grads=False):
+        g = self.m.group
+        nets, strides = [], []
+        for prefix, spec in self._specs():
+            lay, gl, st = [], [], []
+            for i in range(spec.n_layers):
+                W, b = g.view(f'{prefix}{2 * i}.weight'), g.view(f'{prefix}{2 * i}.bias')
+                din, dout = spec.dims[i], spec.dims[i + 1]
+                act = spec.act if i < spec.n_layers - 1 else spec.out_act
+                if member is not None:
+                    W, b = W[member], b[member]
+                    st.append((0, 0))
+                else:
+                    st.append((dout * din, dout))
+                lay.append((W, b, din, dout, ACT_ID[act]))
+                if grads:
+                    gl.append((g.view(f'{prefix}{2 * i}.weight', g.grad), g.view(f'{prefix}{2 * i}.bias', g.grad)))
+            nets.append(Net(lay, gl if grads else None))
+            strides.append(st)
+        return nets, strides
+
+    # ------------------------------------------------------------------ forward
+    def _forward(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False):
+        """Raw head outputs (D, LVR) [Z*n, S+1]; with save=True the activations needed
+        for the backward pass are kept (returns nets too)."""
+        m, L = self.m, _lib.lib()
+        S, A = m.state_dim, m.action_dim
+        S1 = S + 1
+        nets, strides = self._nets(member, grads=save)
+        rows = Z * n
+        if save:
+            for j, net in enumerate(nets):
+                for l, (_, _, din, dout, act) in enumerate(net.layers):
+                    net.sy[l] = self.buf(f'{tag}.sy{j}{l}', rows, dout)
+                    net.sz[l] = self.buf(f'{tag}.sz{j}{l}', rows, dout) if act == ACT_ID['swish'] else None
+                    net.dz[l] = self.buf(f'{tag}.dz{j}{l}', rows, dout)
+            save_x = self.buf(f'{tag}.x', rows, S + A)
+        else:
+            save_x = None
+            nets[1].sy[-1] = self.buf(f'{tag}.D', rows, S1)
+            nets[2].sy[-1] = self.buf(f'{tag}.L', rows, S1)
+        norm = m.state_normalizer
+        d = fill_fwd(nets, [(s, S), (a, A)], n, trunk=True, save_x=save_x, norm=(norm.mean, norm.std), nbatch=Z,
+                     wstride=strides, sstride=[s_zs, a_zs, 0])
+        _lib.check(L.drpo_mlp_forward(ctypes.byref(d), _lib.stream()), 'ensemble forward')
+        return nets, strides, save_x
+
+    def _head(self, D, LVR, s, s_zs, n, Zo, zsel=None, eps=None, noise=None, outputs=('mu', 'lv')):
+        m, L = self.m, _lib.lib()
+        S = m.state_dim
+        out = {}
+        if 'mu' in outputs:
+            out['mu'] = torch.empty(Zo, n, S + 1, device=self.dev)
+            out['lv'] = torch.empty(Zo, n, S + 1, device=self.dev)
+        if 's2' in outputs:
+            out['s2'] = torch.empty(Zo, n, S, device=self.dev)
+            out['r'] = torch.empty(Zo, n, device=self.dev)
+        seed, ctr = (0, 0)
+        if 's2' in outputs and eps is None:
+            nz = self._noise(noise)
+            seed, ctr = nz.seed, nz.next()
+        zs = None
+        if zsel is not None:
+            zs = torch.tensor(list(zsel), dtype=torch.int32, device=self.dev)
+        _lib.check(L.drpo_ens_head(_lib.ptr(D), _lib.ptr(LVR), _lib.ptr(s), s_zs, n, S, Zo, _lib.ptr(m.min_log_var),
+                                   _lib.ptr(m.max_log_var), _lib.ptr(zs), _lib.ptr(eps), seed, ctr,
+                                   _lib.ptr(out.get('mu')), _lib.ptr(out.get('lv')), _lib.ptr(out.get('s2')),
+                                   _lib.ptr(out.get('r')), _lib.stream()), 'ens_head')
+        return out
+
+    def _prep(self, *xs):
+        _lib.require_device(self.m.group.data, *xs)
+        return [x.contiguous().float() for x in xs]
+
+    def forward1(self, s, a, index):
+        s, a = self._prep(s, a)
+        n = s.shape[0]
+        nets, _, _ = self._forward(s, a, n, 1, 0, 0, member=int(index))
+        o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, 0, n, 1)
+        return o['mu'][0], o['lv'][0]
+
+    def forward_all(self, s, a):
+        """s [E|1, n, S], a [E|1, n, A] (leading 1 = shared rows, stride 0)."""
+        s, a = self._prep(s, a)
+        E = self.m.ensemble_size
+        n = s.shape[-2]
+        s_zs = 0 if s.dim() == 2 or s.shape[0] == 1 else n * s.shape[-1]
+        a_zs = 0 if a.dim() == 2 or a.shape[0] == 1 else n * a.shape[-1]
+        if s.dim() == 3:
+            assert s.shape[0] in (1, E) and a.shape[0] in (1, E)
+        nets, _, _ = self._forward(s, a, n, E, s_zs, a_zs)
+        o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, s_zs, n, E)
+        return o['mu'], o['lv']
+
+    def sample(self, s, a, index, noise):
+        s, a = self._prep(s, a)
+        n, S = s.shape
+        eps = None
+        if noise is not None and noise.parity:
+            eps = torch.from_numpy(noise.randn_like((n, S + 1))).to(self.dev)
+        nets, _, _ = self._forward(s, a, n, 1, 0, 0, member=int(index))
+        o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, 0, n, 1, eps=eps, noise=noise, outputs=('s2',))
+        return o['s2'][0], o['r'][0]
+
+    def elite_samples(self, s, a, elites, noise):
+        s, a = self._prep(s, a)
+        n, S = s.shape
+        E = self.m.ensemble_size
+        eps = None
+        if noise is not None and noise.parity:
+            eps = torch.from_numpy(noise.randn_like((len(elites), n, S + 1))).to(self.dev)
+        nets, _, _ = self._forward(s, a, n, E, 0, 0)
+        o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, 0, n, len(elites), zsel=elites, eps=eps, noise=noise,
+                       outputs=('s2',))
+        return o['s2'], o['r']
+
+    # ------------------------------------------------------------------ loss / grads
+    def _loss(self, nets, s, s_zs, t, t_zs, b, Z, grads, gscale=None, loss_out=None, tag='f'):
+        m, L = self.m, _lib.lib()
+        S = m.state_dim
+        S1 = S + 1
+        g = m.group
+        mse = self.buf(f'{tag}.mse', Z)
+        D, LVR = nets[1].sy[-1], nets[2].sy[-1]
+        gD = gL = gmin = gmax = None
+        if grads:
+            gD, gL = self.buf(f'{tag}.gD', Z * b, S1), self.buf(f'{tag}.gL', Z * b, S1)
+            gmin, gmax = g.view('min_log_var', g.grad), g.view('max_log_var', g.grad)
+        _lib.check(L.drpo_ens_loss(_lib.ptr(D), _lib.ptr(LVR), _lib.ptr(s), s_zs, _lib.ptr(t), t_zs, b, S, Z,
+                                   _lib.ptr(m.min_log_var), _lib.ptr(m.max_log_var), float(m.log_var_bound_weight),
+                                   _lib.ptr(gscale), _lib.ptr(mse), _lib.ptr(loss_out), _lib.ptr(gD), _lib.ptr(gL),
+                                   _lib.ptr(gmin), _lib.ptr(gmax), _lib.stream()), 'ens_loss')
+        return mse, gD, gL
+
+    def _backward(self, nets, strides, save_x, gD, gL, b, Z):
+        L = _lib.lib()
+        d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides)
+        _lib.check(L.drpo_mlp_backward(ctypes.byref(d), _lib.stream()), 'ensemble backward')
+        items = []
+        trunk_out = nets[0].sy[-1]
+        for j, net in enumerate(nets):
+            ins = [save_x if j == 0 else trunk_out] + [net.sy[l] for l in range(len(net.layers) - 1)]
+            for l, (W, bb, din, dout, act) in enumerate(net.layers):
+                gW, gb = net.grad_layers[l]
+                it = WgradItem()
+                it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
+                it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
+                it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
+                items.append(it)
+        arr = (WgradItem * len(items))(*items)
+        _lib.check(L.drpo_mlp_wgrad(arr, len(items), _lib.stream()), 'ensemble wgrad')
+
+    def compute_loss_value(self, s, a, t, with_grads=False, gscale=None):
+        """compute_loss on explicit rows (truncated to a multiple of E); returns a 0-d device
+        loss, optionally accumulating the gradients into the group's grad."""
+        s, a, t = self._prep(s, a, t)
+        E = self.m.ensemble_size
+        n = len(t) - len(t) % E
+        b = n // E
+        assert b >= 1, f'compute_loss needs at least {E} rows'
+        S, A = self.m.state_dim, self.m.action_dim
+        s, a, t = s[:n], a[:n], t[:n]
+        loss = torch.empty((), device=self.dev)
+        nets, strides, save_x = self._forward(s, a, b, E, b * S, b * A, tag='cl', save=True)
+        mse, gD, gL = self._loss(nets, s, b * S, t, b * (S + 1), b, E, with_grads, gscale=gscale, loss_out=loss,
+                                 tag='cl')
+        if with_grads:
+            self._backward(nets, strides, save_x, gD, gL, b, E)
+        return loss
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, buffer, steps, noise=None):
+        m, L = self.m, _lib.lib()
+        nz = self._noise(noise)
+        rb = getattr(buffer, '_module', buffer)
+        _lib.require_device(m.group.data, rb._states)
+        n = len(rb)
+        S, A = m.state_dim, m.action_dim
+        S1 = S + 1
+        # Normalizer over the chronological states (physical rows [0, n) hold the same set)
+        m.state_normalizer.fit(rb._states[:n])
+        E, b = m.ensemble_size, m.batch_size
+        rows = E * b
+        xs, xa, xt = self.buf('fit.s', rows, S), self.buf('fit.a', rows, A), self.buf('fit.t', rows, S1)
+        losses = torch.empty(max(steps, 1), device=self.dev)
+        ptr_dev = rb._pointer if rb._host_ptr is None else None
+        ptr_host = rb._host_ptr if rb._host_ptr is not None else 0
+
+        def gather(count, out):
+            idx = nz.randint(n, count) if nz.parity else None
+            idx_t = None if idx is None else torch.from_numpy(idx).to(self.dev)
+            ctr = 0 if nz.parity else nz.next()
+            _lib.check(L.drpo_ens_gather(_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states),
+                                         _lib.ptr(rb._rewards), ptr_host, _lib.ptr(ptr_dev), rb.capacity, count,
+                                         _lib.ptr(idx_t), nz.seed, ctr, S, A, _lib.ptr(out[0]), _lib.ptr(out[1]),
+                                         _lib.ptr(out[2]), _lib.stream()), 'ens_gather')
+
+        for i in range(steps):
+            gather(rows, (xs, xa, xt))
+            m.group.grad.zero_()
+            nets, strides, save_x = self._forward(xs, xa, b, E, b * S, b * A, tag='fit', save=True)
+            _, gD, gL = self._loss(nets, xs, b * S, xt, b * S1, b, E, True, loss_out=losses[i], tag='fit')
+            self._backward(nets, strides, save_x, gD, gL, b, E)
+            m.optimizer.step()
+        # holdout: the same rows for every member (src/dynamics.py:175-183)
+        hb = m.holdout_size
+        assert hb == b, 'reference asserts holdout_size == batch_size (src/dynamics.py:177)'
+        hs, ha, ht = self.buf('ho.s', hb, S), self.buf('ho.a', hb, A), self.buf('ho.t', hb, S1)
+        gather(hb, (hs, ha, ht))
+        nets, _, _ = self._forward(hs, ha, hb, E, 0, 0, tag='ho')
+        mse, _, _ = self._loss(nets, hs, 0, ht, 0, hb, E, False, tag='ho')
+        mse_h = mse.tolist()
+        m.holdout_losses = mse_h
+        m._elite_inds = [int(i) for i in np.argsort(np.asarray(mse_h, np.float32), kind='stable')[:m.num_elites]]
+        return [float(x) for x in losses[:steps].tolist()]
+
+
+    def _gather_buffer(self, rb, count, idx_t, seed, ctr, out):
+        m, L = self.m, _lib.lib()
+        _lib.check(L.drpo_ens_gather(_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states),
+                                     _lib.ptr(rb._rewards), rb.pointer, None, rb.capacity, count, _lib.ptr(idx_t),
+                                     seed, ctr, m.state_dim, m.action_dim, _lib.ptr(out[0]), _lib.ptr(out[1]),
+                                     _lib.ptr(out[2]), _lib.stream()), 'ens_gather')
+
+    def fit_epochs(self, buffer, epochs, max_grad_norm=None, post_epoch_callback=None, post_step_callback=None,
+                   progress_bar=False, verbose=False):
+        """fit(epochs=) == epochal_training over E*epochs epochs of randperm minibatches of
+        E*batch_size rows (src/dynamics.py:185-190, src/train.py:58-100). randperm uses the
+        CPU generator like the reference; the minibatch rows are gathered on the device."""
+        from .optim import grad_sumsq
+        m = self.m
+        rb = getattr(buffer, '_module', buffer)
+        _lib.require_device(m.group.data, rb._states)
+        n = len(rb)
+        S, A = m.state_dim, m.action_dim
+        m.state_normalizer.fit(rb._states[:n])
+        E, tb = m.ensemble_size, m.total_batch_size
+        n_batches = -(-n // tb)
+        losses = []
+        for epoch in range(E * epochs):
+            perm = torch.randperm(n).to(self.dev)
+            ep = torch.empty(n_batches, device=self.dev)
+            for bi in range(n_batches):
+                idx = perm[bi * tb:min(n, (bi + 1) * tb)]
+                cnt = len(idx)
+                xs, xa, xt = self.buf('ep.s', cnt, S), self.buf('ep.a', cnt, A), self.buf('ep.t', cnt, S + 1)
+                self._gather_buffer(rb, cnt, idx, 0, 0, (xs, xa, xt))
+                m.group.grad.zero_()
+                ep_i = ep[bi:bi + 1].view(())
+                loss = self.compute_loss_value(xs, xa, xt, with_grads=True)
+                ep_i.copy_(loss)
+                if max_grad_norm is not None:
+                    part = grad_sumsq(m.group.grad)
+                    sc = m.optimizer.step_scalars()
+                    m.optimizer.apply(m.group.grad, 0, m.group.data.numel(), sc, clip=(part, max_grad_norm))
+                else:
+                    m.optimizer.step()
+                if post_step_callback is not None:
+                    post_step_callback(epoch, bi, n_batches)
+            losses.append(float(np.mean(ep.tolist())))
+            if post_epoch_callback is not None:
+                post_epoch_callback(epoch)
+        return losses
+
+
+class EnsembleLoss(torch.autograd.Function):
+    """compute_loss as a differentiable 0-d tensor for external training loops
+    (src/train.py:58-69 epochal_training: loss.backward(); optimizer.step()).
+    backward() re-runs the fused forward with gradients (scaled by the incoming
+    grad) and accumulates into the flat group's grad (= every parameter's .grad)."""
+
+    @staticmethod
+    def forward(ctx, anchor, engine, s, a, t):
+        ctx.engine, ctx.rows = engine, (s, a, t)
+        return engine.compute_loss_value(s, a, t, with_grads=False)
+
+    @staticmethod
+    def backward(ctx, g):
+        s, a, t = ctx.rows
+        ctx.engine.compute_loss_value(s, a, t, with_grads=True, gscale=g.detach().contiguous().float())
+        return None, None, None, None, None

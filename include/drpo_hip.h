@@ -233,6 +233,26 @@ int drpo_multiplier_head(int64_t B, const float* x, const float* safe_qc, const 
 /* MLPMultiplier.forward output transform (src/ssac.py:107-111) */
 int drpo_multiplier_out(int64_t B, const float* x, float upper_bound, float* lam, drpo_stream_t stream);
 
+/* ---------------------------------------------------------------- dynamics ensemble
+ * BatchedGaussianEnsemble (src/dynamics.py:112-253); the MLP passes use
+ * drpo_mlp_forward/backward/wgrad with nbatch = ensemble members.              */
+/* fit / holdout minibatch gather by chronological replay index (src/dynamics.py:156-166,
+ * 175-177); idx NULL -> Philox randint(n) with (seed, ctr); ptr_dev overrides ptr */
+int drpo_ens_gather(const float* states, const float* actions, const float* next_states, const float* rewards,
+                    int64_t ptr, const int64_t* ptr_dev, int64_t cap, int64_t rows, const int64_t* idx, uint64_t seed,
+                    uint64_t ctr, int S, int A, float* xs, float* xa, float* xt, drpo_stream_t stream);
+/* mu = diff + [s, 0], soft log-var clamp, optional sample -> (s', r)
+ * (_forward1 / _forward_all / sample / elite_samples, src/dynamics.py:112-134,198-234) */
+int drpo_ens_head(const float* D, const float* LVR, const float* s, int64_t s_zstride, int64_t n, int S, int nz_out,
+                  const float* minlv, const float* maxlv, const int* zsel, const float* eps, uint64_t seed,
+                  uint64_t ctr, float* mu, float* lv, float* s2, float* r, drpo_stream_t stream);
+/* per-member NLL (_mse_loss, src/dynamics.py:236-253), total compute_loss (:143-153)
+ * and, when gD != NULL, its gradients (scaled by *gscale if given) */
+int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
+                  int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv, float weight,
+                  const float* gscale, float* mse, float* loss, float* gD, float* gLVR, float* gmin, float* gmax,
+                  drpo_stream_t stream);
+
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam (coupled L2), clip_grad_norm_, update_ema (src/ssac.py:446-455,
  * src/torch_util.py:223-226), over flat parameter groups                       */
