@@ -115,7 +115,7 @@ class CriticHead(ctypes.Structure):
     """drpo_critic_head_t"""
     _fields_ = [('B', c_int64), ('C', c_int), ('distributional', c_int), ('deterministic_backup', c_int),
                 ('discount', c_float), ('qc_td_bound', c_float), ('lmin', c_float), ('lmax', c_float),
-                ('log_alpha', P), ('r', P), ('h', P), ('d', P), ('q0t', P), ('q1t', P), ('logp2', P),
+                ('log_alpha', P), ('r', P), ('h', P), ('d', P), ('dc', P), ('q0t', P), ('q1t', P), ('logp2', P),
                 ('mu_t', P), ('ls_t', P), ('eps3', P), ('seed', c_uint64), ('ctr', c_uint64),
                 ('q0', P), ('q1', P), ('mu', P), ('ls', P), ('dq0', P), ('dq1', P), ('dmu', P), ('dls', P),
                 ('loss', P)]
@@ -129,6 +129,7 @@ PROTOTYPES.update({
                                   c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
     'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,
                                  P]),
+    'drpo_cc_dist': (c_int, [P, P, c_int64, c_int, c_float, c_float, c_float, P, c_uint64, c_uint64, P, P, P]),
     'drpo_cc_head': (c_int, [P, P, c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P]),
     'drpo_critic_head': (c_int, [POINTER(CriticHead), P]),
     'drpo_actor_upstream': (c_int, [c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P, P, P, P, P, P, P, P,

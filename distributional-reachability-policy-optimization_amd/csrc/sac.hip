@@ -135,6 +135,11 @@ __global__ void policy_head_kernel(const float* raw, int64_t B, int A, int mode,
     const float ls = -6.f + 10.f * sigmoidf(raw[i * 2 * A + A + d]);
     const float sd = expf(ls) * 1.0f;
     if (amean) amean[i * A + d] = tanhf(mu);
+    if (mode == 3) {   // distribution parameters (loc, scale) for distr()
+      if (u_out) u_out[i * A + d] = mu;
+      if (e_out) e_out[i * A + d] = sd;
+      continue;
+    }
     if (mode == 2) continue;
     const float e = normal_at(eps, i * A + d, seed, ctr, site);
     const float u = (mode == 0) ? e * sd + mu : mu + e * sd;
@@ -146,14 +151,14 @@ __global__ void policy_head_kernel(const float* raw, int64_t B, int A, int mode,
     const float base = -((u - mu) * (u - mu)) / (2.f * (sd * sd)) - logf(sd) - 0.91893853320467274f;
     lp += (0.f - ladj) + base;
   }
-  if (logp && mode != 2) logp[i] = lp;
+  if (logp && mode < 2) logp[i] = lp;
 }
 
 DRPO_API int drpo_policy_head(const float* raw, int64_t B, int A, int mode, const float* eps, uint64_t seed,
                               uint64_t ctr, uint32_t site, float* a, float* logp, float* u, float* e, float* amean,
                               drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
-  DRPO_REQUIRE(mode >= 0 && mode <= 2 && A >= 1, "drpo_policy_head: bad mode/A");
+  DRPO_REQUIRE(mode >= 0 && mode <= 3 && A >= 1, "drpo_policy_head: bad mode/A");
   if (B == 0) return DRPO_OK;
   policy_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(raw, B, A, mode, eps, seed, ctr, site, a, logp,
                                                                       u, e, amean);
@@ -189,6 +194,36 @@ DRPO_API int drpo_cc_head(const float* mu, const float* lsraw, int64_t B, int C,
   return DRPO_OK;
 }
 
+// ConstraintCritic.forward outputs per constraint (src/ssac.py:75-92): mode 0
+// (uncertainty) q = mu + std_ratio*std; mode 1 (sample) std and
+// q = mu + clamp(eps, -2, 2)*std. n = rows*C elements.
+__global__ void cc_dist_kernel(const float* mu, const float* lsraw, int64_t n, int mode, float std_ratio, float lmin,
+                               float lmax, const float* eps, uint64_t seed, uint64_t ctr, float* std_out, float* q) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float sd = cc_std(lsraw[i], lmin, lmax);
+  if (mode == 0) {
+    q[i] = mu[i] + std_ratio * sd;
+  } else {
+    float e = normal_at(eps, i, seed, ctr, 0xcc01u);
+    e = fminf(fmaxf(e, -2.f), 2.f);
+    if (std_out) std_out[i] = sd;
+    q[i] = mu[i] + e * sd;
+  }
+}
+
+DRPO_API int drpo_cc_dist(const float* mu, const float* lsraw, int64_t n, int mode, float std_ratio,
+                          float log_std_min, float log_std_max, const float* eps, uint64_t seed, uint64_t ctr,
+                          float* std_out, float* q, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(mu && lsraw && q && n >= 0 && (mode == 0 || mode == 1), "drpo_cc_dist: bad arguments");
+  if (n == 0) return DRPO_OK;
+  cc_dist_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(mu, lsraw, n, mode, std_ratio, log_std_min,
+                                                                  log_std_max, eps, seed, ctr, std_out, q);
+  DRPO_LAUNCH_CHECK("cc_dist");
+  return DRPO_OK;
+}
+
 // ---------------------------------------------------------------------------
 // critic + certificate targets, losses, gradients (update_critic)
 // ---------------------------------------------------------------------------
@@ -203,6 +238,9 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
     float nv = fminf(p.q0t[i], p.q1t[i]);
     if (!p.deterministic_backup) nv = nv - alpha * p.logp2[i];
     const float dn = p.d[i] ? 1.f : 0.f;
+    // certificate-target done flags: the batch's, or the model-predicted ones of the
+    // robust branch (src/ssac.py:387-400)
+    const float dnc = p.dc ? (p.dc[i] ? 1.f : 0.f) : dn;
     const float y = p.r[i] + p.discount * (1.f - dn) * nv;
     const float e0 = p.q0[i] - y, e1 = p.q1[i] - y;
     const float invB = 1.f / (float)p.B;
@@ -222,7 +260,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
         q2 = p.mu_t[k];
       }
       const float nonterm = (1.f - p.discount) * hv + p.discount * fmaxf(hv, q2);
-      const float yc = nonterm * (1.f - dn) + hv * dn;
+      const float yc = nonterm * (1.f - dnc) + hv * dnc;
       if (p.distributional) {
         const float diff = fminf(fmaxf(yc - mu, -p.qc_td_bound), p.qc_td_bound);
         const float yb = diff + mu;

@@ -101,10 +101,12 @@ class EnsembleEngine:
         _lib.check(L.drpo_mlp_forward(ctypes.byref(d), _lib.stream()), 'ensemble forward')
         return nets, strides, save_x
 
-    def _head(self, D, LVR, s, s_zs, n, Zo, zsel=None, eps=None, noise=None, outputs=('mu', 'lv')):
+    def _head(self, D, LVR, s, s_zs, n, Zo, zsel=None, eps=None, noise=None, outputs=('mu', 'lv'), out=None):
         m, L = self.m, _lib.lib()
         S = m.state_dim
-        out = {}
+        if out is not None:
+            outputs = ()
+        out = {} if out is None else out
         if 'mu' in outputs:
             out['mu'] = torch.empty(Zo, n, S + 1, device=self.dev)
             out['lv'] = torch.empty(Zo, n, S + 1, device=self.dev)
@@ -112,7 +114,7 @@ class EnsembleEngine:
             out['s2'] = torch.empty(Zo, n, S, device=self.dev)
             out['r'] = torch.empty(Zo, n, device=self.dev)
         seed, ctr = (0, 0)
-        if 's2' in outputs and eps is None:
+        if 's2' in out and eps is None:
             nz = self._noise(noise)
             seed, ctr = nz.seed, nz.next()
         zs = None
@@ -148,15 +150,16 @@ class EnsembleEngine:
         o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, s_zs, n, E)
         return o['mu'], o['lv']
 
-    def sample(self, s, a, index, noise):
+    def sample(self, s, a, index, noise, eps=None, out=None, tag='f'):
+        """sample (src/dynamics.py:198-203) for member ``index``. eps: recorded draws
+        (device tensor) or None (tape / Philox); out: optional {'s2', 'r'} buffers."""
         s, a = self._prep(s, a)
         n, S = s.shape
-        eps = None
-        if noise is not None and noise.parity:
+        if eps is None and noise is not None and noise.parity:
             eps = torch.from_numpy(noise.randn_like((n, S + 1))).to(self.dev)
-        nets, _, _ = self._forward(s, a, n, 1, 0, 0, member=int(index))
-        o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, 0, n, 1, eps=eps, noise=noise, outputs=('s2',))
-        return o['s2'][0], o['r'][0]
+        nets, _, _ = self._forward(s, a, n, 1, 0, 0, member=int(index), tag=tag)
+        o = self._head(nets[1].sy[-1], nets[2].sy[-1], s, 0, n, 1, eps=eps, noise=noise, outputs=('s2',), out=out)
+        return o['s2'].reshape(n, S), o['r'].reshape(n)
 
     def elite_samples(self, s, a, elites, noise):
         s, a = self._prep(s, a)

@@ -195,3 +195,137 @@ def normalize(x, mean, std, eps):
     _lib.check(L.drpo_normalize(_lib.ptr(x), _lib.ptr(mean), _lib.ptr(std), float(eps), _lib.ptr(y),
                                 x.numel() // S, S, _lib.stream()), 'normalize')
     return y
+
+
+# ---------------------------------------------------------------------------
+# stand-alone network forwards (policy act/distr, critics, multiplier): one fused
+# MLP launch + one head launch each. Used outside the fused SAC step (real-env
+# acting, evaluation, diagnostics) -- src/policy.py:76-100, src/ssac.py:17-111.
+# ---------------------------------------------------------------------------
+_default_noise = None
+
+
+def default_noise():
+    global _default_noise
+    if _default_noise is None:
+        from .rng import DeviceNoise
+        _default_noise = DeviceNoise(torch.initial_seed() ^ 0xAC7)
+    return _default_noise
+
+
+def _mlp(nets, srcs, rows, trunk=False, norm=None):
+    from .sac_step import fill_fwd
+    L = _lib.lib()
+    d = fill_fwd(nets, srcs, rows, trunk=trunk, norm=norm)
+    _lib.check(L.drpo_mlp_forward(ctypes.byref(d), _lib.stream()), 'mlp_forward')
+
+
+def _net(group, prefix, spec, out_rows=None):
+    from .sac_step import Net, spec_layers
+    net = Net(spec_layers(group, prefix, spec))
+    if out_rows is not None:
+        net.sy[-1] = torch.empty(out_rows, net.dout, device=group.data.device)
+    return net
+
+
+def _flat2(x, dim):
+    x = x.contiguous().float()
+    return x.reshape(-1, dim), x.shape[:-1]
+
+
+def policy_raw(policy, states):
+    _lib.require_device(policy.group.data, states)
+    s, lead = _flat2(states, policy.state_dim)
+    net = _net(policy.group, 'net.', policy.spec, len(s))
+    _mlp([net], [(s, policy.state_dim)], len(s))
+    return net.sy[-1], lead
+
+
+def policy_act(policy, states, eval, noise=None):
+    """TorchPolicy.act (src/policy.py:76-79): eval -> tanh(mu), else distr.sample()."""
+    L = _lib.lib()
+    raw, lead = policy_raw(policy, states)
+    n, A = raw.shape[0], policy.action_dim
+    a = torch.empty(n, A, device=raw.device)
+    if eval:
+        _lib.check(L.drpo_policy_head(_lib.ptr(raw), n, A, 2, None, 0, 0, 0, None, None, None, None, _lib.ptr(a),
+                                      _lib.stream()), 'policy_head')
+    else:
+        noise = default_noise() if noise is None else noise
+        eps = noise.normal((n, A))
+        eps_t = None if eps is None else _dev(eps, raw.device)
+        _lib.check(L.drpo_policy_head(_lib.ptr(raw), n, A, 0, _lib.ptr(eps_t), noise.seed, noise.next(), 9,
+                                      _lib.ptr(a), None, None, None, None, _lib.stream()), 'policy_head')
+    return a.reshape(*lead, A)
+
+
+def policy_params(policy, states):
+    """(loc, scale) of the squashed Gaussian (src/policy.py:88-97)."""
+    L = _lib.lib()
+    raw, lead = policy_raw(policy, states)
+    n, A = raw.shape[0], policy.action_dim
+    mu, sd = torch.empty(n, A, device=raw.device), torch.empty(n, A, device=raw.device)
+    _lib.check(L.drpo_policy_head(_lib.ptr(raw), n, A, 3, None, 0, 0, 0, None, None, _lib.ptr(mu), _lib.ptr(sd),
+                                  None, _lib.stream()), 'policy_head')
+    return mu.reshape(*lead, A), sd.reshape(*lead, A)
+
+
+def critic_all(critic, state, action, which=None):
+    """CriticEnsemble.all (src/ssac.py:30-32): every Q net in one launch (grid.y = net);
+    ``which`` restricts to a subset (random_choice, :38-40)."""
+    _lib.require_device(critic.group.data, state, action)
+    s, lead = _flat2(state, state.shape[-1])
+    a, _ = _flat2(action, action.shape[-1])
+    n = len(s)
+    which = range(critic.n_critics) if which is None else which
+    nets = [_net(critic.group, f'{critic.prefix}qs.{i}.', critic.spec, n) for i in which]
+    for k in range(0, len(nets), 3):
+        _mlp(nets[k:k + 3], [(s, s.shape[1]), (a, a.shape[1])], n)
+    return [net.sy[-1].reshape(*lead) for net in nets]
+
+
+def constraint_critic_forward(cc, state, action, uncertainty=False, sample=False, noise=None):
+    """ConstraintCritic.forward (src/ssac.py:64-92): trunk + both heads in one launch,
+    then the log-std clamp / quantile bound / clipped sample."""
+    assert not (uncertainty and sample), 'Uncertainty bound and sample cannot be True simultaneously.'
+    L = _lib.lib()
+    _lib.require_device(cc.group.data, state, action)
+    s, lead = _flat2(state, state.shape[-1])
+    a, _ = _flat2(action, action.shape[-1])
+    n, C = len(s), cc.output_dim
+    trunk = _net(cc.group, cc.prefix + 'trunk.', cc.trunk_spec)
+    mean = _net(cc.group, cc.prefix + 'mean_head.', cc.mean_spec, n)
+    nets = [trunk, mean]
+    if uncertainty or sample:
+        nets.append(_net(cc.group, cc.prefix + 'log_std_head.', cc.logstd_spec, n))
+    _mlp(nets, [(s, s.shape[1]), (a, a.shape[1])], n, trunk=True)
+    shape = (*lead, C) if C > 1 else tuple(lead)
+    mu = mean.sy[-1]
+    if not (uncertainty or sample):
+        return mu.reshape(shape)
+    noise = default_noise() if noise is None else noise
+    eps = noise.randn_like((n, C) if C > 1 else (n,), used=sample)
+    eps_t = None if eps is None else _dev(eps, mu.device).reshape(n, C)
+    q = torch.empty(n, C, device=mu.device)
+    sd = torch.empty(n, C, device=mu.device) if sample else None
+    _lib.check(L.drpo_cc_dist(_lib.ptr(mu), _lib.ptr(nets[2].sy[-1]), n * C, 1 if sample else 0, float(cc.std_ratio),
+                              float(cc.log_std_min), float(cc.log_std_max), _lib.ptr(eps_t), noise.seed,
+                              noise.next(), _lib.ptr(sd), _lib.ptr(q), _lib.stream()), 'cc_dist')
+    if uncertainty:
+        return q.reshape(shape)
+    return mu.reshape(shape), sd.reshape(shape), q.reshape(shape)
+
+
+def multiplier_forward(mult, state, Qc):
+    """MLPMultiplier.forward (src/ssac.py:106-111)."""
+    L = _lib.lib()
+    _lib.require_device(mult.group.data, state, Qc)
+    s, lead = _flat2(state, state.shape[-1])
+    q = Qc.contiguous().float().reshape(-1, 1)
+    n = len(s)
+    net = _net(mult.group, 'lam.', mult.spec, n)
+    _mlp([net], [(s, s.shape[1]), (q, 1)], n)
+    lam = torch.empty(n, device=s.device)
+    _lib.check(L.drpo_multiplier_out(n, _lib.ptr(net.sy[-1]), float(mult.upper_bound), _lib.ptr(lam), _lib.stream()),
+               'multiplier_out')
+    return lam.reshape(*lead)

@@ -8,6 +8,22 @@ from .params import FlatGroup, MLPSpec
 from .torch_util import Module
 
 
+class SquashedGaussian(torch.distributions.transformed_distribution.TransformedDistribution):
+    """src/squashed_gaussian.py:7-16 (Normal pushed through TanhTransform(cache_size=1))."""
+
+    def __init__(self, loc, scale, validate_args=None):
+        from torch.distributions import Normal
+        from torch.distributions.transforms import TanhTransform
+        super().__init__(Normal(loc, scale), TanhTransform(cache_size=1), validate_args=validate_args)
+
+    @property
+    def mean(self):
+        mu = self.base_dist.loc
+        for t in self.transforms:
+            mu = t(mu)
+        return mu
+
+
 class SquashedGaussianPolicy(Module):
     def __init__(self, state_dim, action_dim, hidden_dim=256, hidden_layers=2, group=None, prefix='net.',
                  log_std_bounds=(-6, 4), std_multiplier=1.0):
@@ -38,9 +54,18 @@ class SquashedGaussianPolicy(Module):
         from .params import layer_views
         return layer_views(self.group, 'net.', self.spec, buf)
 
-    def act(self, states, eval):
+    def act(self, states, eval, noise=None):
+        """TorchPolicy.act (src/policy.py:76-79): fused MLP + squashed-Gaussian head."""
         from . import ops
-        return ops.policy_act(self, states, eval)
+        return ops.policy_act(self, states, eval, noise)
+
+    def distr(self, states):
+        """Independent(SquashedGaussian(mu, std), 1) (src/policy.py:69-70,88-97); loc/scale
+        come from the fused kernels, the distribution object is torch's."""
+        from . import ops
+        from torch import distributions as td
+        mu, std = ops.policy_params(self, states)
+        return td.Independent(SquashedGaussian(mu, std), 1)
 
     def act1(self, state, eval=False):
         return self.act(torch.unsqueeze(state, 0), eval)[0]

@@ -119,6 +119,9 @@ class SACEngine:
         self.sol = solver
         self.S, self.A, self.C = solver.state_dim, solver.action_dim, solver.con_dim
         self.dev = solver.actor.group.data.device
+        from .envs import device_env_params
+        self.env_params = device_env_params(solver.env) if solver.qc_under_uncertainty and \
+            not solver.distributional_qc else None
         self.B = None
         self.ws = {}
         self.loss_pool = None
@@ -189,7 +192,7 @@ class SACEngine:
         self.br, self.bh = buf('b.r', B), buf('b.h', B, C)
         self.bd, self.bv = buf('b.d', B, dtype=torch.uint8), buf('b.v', B, dtype=torch.uint8)
         # noise buffers (parity mode)
-        for k, shp in (('e1', (B, A)), ('e2', (B, A)), ('e3', (B, C)), ('e5', (B, A)), ('e6', (B, A)),
+        for k, shp in (('em', (B, S + 1)), ('e1', (B, A)), ('e2', (B, A)), ('e3', (B, C)), ('e5', (B, A)), ('e6', (B, A)),
                        ('e7', (B, A))):
             buf(k, *shp)
         buf('idx_r', B, dtype=torch.int64)
@@ -269,10 +272,15 @@ class SACEngine:
         self.noise = noise = noise or self.noise
         L = _lib.lib()
         dist = sol.distributional_qc and sol.qc_under_uncertainty
-        if sol.qc_under_uncertainty and not sol.distributional_qc:
-            raise NotImplementedError('robust (model-sampled) certificate target: see DESIGN.md (next)')
+        robust = sol.qc_under_uncertainty and not sol.distributional_qc
         qshape = (B,) if C == 1 else (B, C)
         e1 = self._eps('e1', noise.normal((B, A)))
+        if robust:
+            # robust certificate target (src/ssac.py:387-400): s' drawn from one elite
+            # member of the dynamics model, done flags from the env's constraint fns
+            model = sol.model_ensemble
+            member = model._elite_inds[noise.choice(len(model._elite_inds))]
+            em = self._eps('em', noise.randn_like((B, S + 1)))
         e2 = self._eps('e2', noise.normal((B, A)))
         e3 = self._eps('e3', noise.randn_like(qshape)) if dist else None
         noise.randn_like(qshape, used=False)       # loss forward's unused draw (src/ssac.py:80)
@@ -283,12 +291,23 @@ class SACEngine:
                                                   [(self.bs2, S), (None, 0), (None, 0)], B))
         self._policy_head(ws['c.raw_a'], 0, e1, SITE_PI_NEXT, ctr, a=self.buf('c.a2', B, A), logp=self.buf('c.lp2', B))
         self._run_fwd('c.qt', lambda: fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (ws['c.a2'], A), (None, 0)], B))
-        # safe policy sample on s'
-        self._run_fwd('c.safe', lambda: fill_fwd([self._out_net(n['safe'], 'c.raw_s', B)],
-                                                 [(self.bs2, S), (None, 0), (None, 0)], B))
+        # safe policy sample on s' (robust: on the model's s')
+        s2c, rk = self.bs2, ''
+        if robust:
+            s2c, rk = self.buf('c.s2m', B, S), '.r'
+            model.engine.sample(self.bs, self.ba, member, noise, eps=em, tag='sac',
+                                out={'s2': s2c, 'r': self.buf('c.r2m', B)})
+            dm = self.buf('c.dm', B, dtype=torch.uint8)
+            ep = self.env_params
+            _lib.check(L.drpo_env_constraints(ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr'],
+                                              ep['quad_x_threshold'], ep['quad_z_threshold'], s2c.data_ptr(), B, S,
+                                              dm.data_ptr(), self.buf('c.vm', B, dtype=torch.uint8).data_ptr(),
+                                              self.buf('c.hm', B, C).data_ptr(), _lib.stream()), 'env_constraints')
+        self._run_fwd('c.safe' + rk, lambda: fill_fwd([self._out_net(n['safe'], 'c.raw_s', B)],
+                                                      [(s2c, S), (None, 0), (None, 0)], B))
         self._policy_head(ws['c.raw_s'], 0, e2, SITE_SAFE_NEXT, ctr, a=self.buf('c.a2s', B, A))
-        self._run_fwd('c.cct', lambda: fill_fwd(self._cc_nets('t'), [(self.bs2, S), (ws['c.a2s'], A), (None, 0)], B,
-                                                trunk=True))
+        self._run_fwd('c.cct' + rk, lambda: fill_fwd(self._cc_nets('t'), [(s2c, S), (ws['c.a2s'], A), (None, 0)], B,
+                                                     trunk=True))
         # critics and constraint critic at (s, a) with saves
         xs = self.buf('c.x', B, S + A)
         self._run_fwd('c.q', lambda: fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B,
@@ -314,6 +333,7 @@ class SACEngine:
         ch.lmin, ch.lmax = cc.log_std_min, cc.log_std_max
         ch.log_alpha = sol.log_alpha.data_ptr()
         ch.eps3 = _p(e3)
+        ch.dc = ws['c.dm'].data_ptr() if robust else 0
         ch.seed, ch.ctr = noise.seed, ctr
         ch.loss = loss.data_ptr()
         _lib.check(L.drpo_critic_head(ctypes.byref(ch), _lib.stream()), 'critic_head')

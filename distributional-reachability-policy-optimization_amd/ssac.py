@@ -55,9 +55,11 @@ class CriticEnsemble(Configurable, Module):
         qs = self.all(state, action)
         return sum(qs) / len(qs)
 
-    def random_choice(self, state, action):
+    def random_choice(self, state, action, noise=None):
         import random
-        return self.all(state, action)[random.choice(range(self.n_critics))]
+        from . import ops
+        i = random.choice(range(self.n_critics)) if noise is None else noise.choice(self.n_critics)
+        return ops.critic_all(self, state, action, which=[i])[0]
 
 
 class ConstraintCritic(Configurable, Module):
@@ -98,9 +100,9 @@ class ConstraintCritic(Configurable, Module):
         self.mean_head = self.mean_spec.build(g, prefix + 'mean_head.')
         self.log_std_head = self.logstd_spec.build(g, prefix + 'log_std_head.')
 
-    def forward(self, state, action, uncertainty=False, sample=False):
+    def forward(self, state, action, uncertainty=False, sample=False, noise=None):
         from . import ops
-        return ops.constraint_critic_forward(self, state, action, uncertainty, sample)
+        return ops.constraint_critic_forward(self, state, action, uncertainty, sample, noise)
 
 
 class MLPMultiplier(Configurable, Module):
@@ -244,8 +246,8 @@ class SSAC(Module):
         self._engine = None
 
     # ------------------------------------------------------------------
-    def act(self, states, eval):
-        return self.actor.act(states, eval)
+    def act(self, states, eval, noise=None):
+        return self.actor.act(states, eval, noise)
 
     @property
     def alpha(self):

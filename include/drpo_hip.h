@@ -182,9 +182,15 @@ int drpo_sample_batch(const drpo_buffer_view_t* real, const drpo_buffer_view_t* 
                       float* a, float* s2, float* r, uint8_t* d, uint8_t* v, float* h, drpo_stream_t stream);
 
 /* squashed Gaussian (src/policy.py:89-97, src/squashed_gaussian.py): mode 0 sample,
- * 1 rsample, 2 mean (tanh(mu)); raw = [mu | log-std pre-activation] [B][2A] */
+ * 1 rsample, 2 mean (tanh(mu)), 3 distribution parameters (loc -> u, scale -> e); raw = [mu | log-std pre-activation] [B][2A] */
 int drpo_policy_head(const float* raw, int64_t B, int A, int mode, const float* eps, uint64_t seed, uint64_t ctr,
                      uint32_t site, float* a, float* logp, float* u, float* e, float* amean, drpo_stream_t stream);
+
+/* ConstraintCritic.forward per-constraint outputs (src/ssac.py:75-92): mode 0 uncertainty
+ * q = mu + std_ratio*std, mode 1 sample (std, mu + clamp(eps, +-2)*std); eps NULL -> Philox */
+int drpo_cc_dist(const float* mu, const float* lsraw, int64_t n, int mode, float std_ratio, float log_std_min,
+                 float log_std_max, const float* eps, uint64_t seed, uint64_t ctr, float* std_out, float* q,
+                 drpo_stream_t stream);
 
 /* ConstraintCritic log-std clamp + quantile bound mu + std_ratio*std, max over C
  * (src/ssac.py:64-92, _get_qc :588-600) */
@@ -199,6 +205,7 @@ typedef struct {
   const float* log_alpha;
   const float *r, *h;
   const uint8_t* d;
+  const uint8_t* dc;    /* certificate-target done flags (robust branch: model-predicted); NULL = d */
   const float *q0t, *q1t, *logp2;
   const float *mu_t, *ls_t;
   const float* eps3;

@@ -351,9 +351,16 @@ def gen_ssac(out, name, seed, tag, distributional, uncertainty):
     alg = build_alg(name, cfg, seed)
     sol = alg.solver
     d = meta(name, cfg, alg)
+    rng = np.random.RandomState(seed + 5)
+    if uncertainty and not distributional:
+        # robust certificate target samples the dynamics model inside update_critic
+        # (src/ssac.py:387-400): give it fitted normalizer stats and elites first
+        m = alg.model_ensemble
+        m.state_normalizer.fit(torch.from_numpy(synth_states(name, 500, rng)))
+        m._elite_inds = [2, 0, 1]
+        d['model/elite_inds'] = np.array(m._elite_inds)
     d.update(sd_dict(sol, 'sd0/'))
     d['sd0/log_alpha'] = t2n(sol.log_alpha)
-    rng = np.random.RandomState(seed + 5)
     batch = synth_batch(alg, name, cfg.sac_cfg.batch_size, rng)
     # the reference preprocesses in SMBPO.update_solver; feed preprocessed values directly
     for i, nm in enumerate(['s', 'a', 's2', 'r', 'd', 'v', 'h']):
@@ -425,6 +432,10 @@ def main():
     out = HERE
     tmp = tempfile.mkdtemp()
     default_log.setup(tmp)
+    if sys.argv[1:] == ['robust']:
+        gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
+        gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
+        return
     gen_constraints(out)
     gen_init_hashes(out)
     for name, seed in [('point-robot', 11), ('quadrotor', 12)]:
@@ -434,6 +445,8 @@ def main():
     gen_ssac(out, 'point-robot', 31, 'drpo_point', True, True)
     gen_ssac(out, 'quadrotor', 32, 'drpo_quad', True, True)
     gen_ssac(out, 'quadrotor', 33, 'vanilla_quad', False, False)
+    gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
+    gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
     gen_smbpo_update(out, 'point-robot', 41)
     gen_smbpo_update(out, 'quadrotor', 42)
     print('golden fixtures written to', out)

@@ -33,7 +33,7 @@ def check_params(module, ref, msg, skip=('model_ensemble', 'total_updates', 'log
     assert not bad, f'{msg}: {bad[:6]}'
 
 
-@pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad'])
+@pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point'])
 def test_ssac_updates_match_reference(tag):
     d = load_golden(f'ssac_{tag}')
     env = str(d['meta/env'])
@@ -43,6 +43,8 @@ def test_ssac_updates_match_reference(tag):
     sol.log_alpha.fill_(float(sd0.pop('log_alpha')))
     missing, unexpected = sol.load_state_dict(sd0, strict=False)
     assert not unexpected
+    if 'model/elite_inds' in d.files:     # robust branch samples the dynamics model
+        alg.model_ensemble._elite_inds = list(d['model/elite_inds'])
     batch = [torch.from_numpy(d['in/' + k]).to(DEV) for k in ['s', 'a', 's2', 'r', 'd', 'v', 'h']]
     tape = drpo_amd.TapeNoise.from_npz(d, 'critic_tape')
     lq, lqc = sol.update_critic(*batch, noise=tape)
