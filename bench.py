@@ -38,6 +38,20 @@ def rollout_flop_per_transition(S, A, Ha=256, Hm=200):
     return 2 * ((S * Ha + Ha * Ha + Ha * 2 * A) + ((S + A) * Hm + 3 * Hm * Hm + 2 * Hm * (S + 1)))
 
 
+def sac_flop_per_step(B, S=12, A=2, C=2, H=256):
+    """per-sample MACs of one update_solver at the rollout_and_update
+    cadence (critic every step, actor 1/2, multiplier 1/5), backward = 2x forward."""
+    Fpi = S * H + H * H + H * 2 * A
+    Fq = (S + A) * H + H * H + H
+    Fqc = (S + A) * H + H * H + 2 * (H * H + H * C)
+    Fqcm = (S + A) * H + H * H + H * H + H * C
+    Fl = (S + 1) * H + H * H + H
+    critic = 2 * Fpi + 8 * Fq + 4 * Fqc + Fqcm
+    actor = 7 * Fpi + 3 * Fq + 7 * Fqc + Fl
+    mult = 2 * Fpi + 2 * Fqc + 3 * Fl
+    return 2 * B * (critic + actor / 2 + mult / 5)
+
+
 def synth_replay(S, A, C, N, rng):
     s = rng.normal(0, 0.1, size=(N, S)).astype(np.float32)
     s[:, 0] = rng.uniform(-1, 1, N)
@@ -106,9 +120,34 @@ def cpu_baseline(B, H, E, seed, budget_s=12.0):
         n_tr += len(out['states'])
         reps += 1
     roll_tps = n_tr / (time.perf_counter() - t0)
+    # SAC: oracle update_critic / update_actor_and_alpha / update_multiplier at the
+    # rollout_and_update cadence on batches drawn from the same synthetic replay
+    Ps = {k[len('solver.'):]: v for k, v in sd.items() if k.startswith('solver.') and
+          not k.startswith('solver.model_ensemble') and k != 'solver.total_updates'}
+    orc = O.SSACOracle(Ps, dict(batch_size=B, target_entropy=-2.0, penalty_lb=-1.0, actor_lr=1e-4,
+                                updates_per_training=100 * 360 * 10), 2, 2)
+    live = O.LiveRNG()
+    r = torch.from_numpy(rep['rewards'])
+    hcv = torch.from_numpy(rep['constraint_values'])
+    t1, steps = time.perf_counter(), 0
+    while time.perf_counter() - t1 < budget_s / 2 or steps < 2:
+        idx = torch.randint(len(st), [B])
+        batch = (st[idx], torch.from_numpy(rep['actions'])[idx], torch.from_numpy(rep['next_states'])[idx],
+                 r[idx] * 2.0 + 2.0, torch.zeros(B, dtype=torch.bool), torch.zeros(B, dtype=torch.bool),
+                 hcv[idx] * 10.0 + (hcv[idx] > 0).float() * 0.5)
+        orc.update_critic(*batch, live)
+        if steps % 2 == 0:
+            orc.update_actor_and_alpha(batch[0], live)
+        if steps % 5 == 0:
+            orc.update_multiplier(batch[0], live)
+        steps += 1
+    sac_sps = steps / (time.perf_counter() - t1)
     return {'value': roll_tps, 'unit': 'imagined transitions/s', 'cores': threads, 'kind': 'port',
             'sample': f'{reps} x oracle SMBPO.rollout (quadrotor B={B} H={H} E={E}, steady mode) on the host CPU '
-                      f'(torch {torch.__version__}, {threads} threads)'}
+                      f'(torch {torch.__version__}, {threads} threads)',
+            'sac': {'value': sac_sps, 'unit': f'grad-steps/s of B={B} samples',
+                    'sample': f'{steps} x oracle update_solver cadence (critic; actor 1/2; multiplier 1/5), '
+                              f'B={B}, {threads} threads'}}
 
 
 def main():
@@ -143,6 +182,8 @@ def main():
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     steady_mode(alg)
+    from drpo_amd.distributed import sync_parameters
+    sync_parameters(alg)            # every rank starts from rank 0's weights (DP replicas)
     do_sac = not args.rollout_only
     if do_sac:
         try:
@@ -215,10 +256,13 @@ def main():
         'config': {'workload': 'quadrotor E=7 H=10 B=4096 (BASELINE configs[1])', 'env': 'quadrotor',
                    'ensemble': E, 'horizon': H, 'batch': B, 'global_batch': B * world,
                    'parallelism': f'dp{world}' if world > 1 else 'single', 'drpo_flags': True},
-        'sac': {'metric': 'SAC grad-steps/sec', 'value': (alg.solver_updates_per_step * args.steps * world / sac_s)
+        'sac': {'metric': 'SAC grad-steps/sec', 'unit': f'grad-steps/s of B={B} samples (whole job)',
+                'value': (alg.solver_updates_per_step * args.steps * world / sac_s) if do_sac and sac_s > 0 else None,
+                'global_steps_per_s': (alg.solver_updates_per_step * args.steps / sac_s)
                 if do_sac and sac_s > 0 else None,
-                'per_rank_value': (alg.solver_updates_per_step * args.steps / sac_s) if do_sac and sac_s > 0 else None,
-                'measured': do_sac},
+                'global_batch': B * world, 'gradient_exchange': 'RCCL all-reduce (mean) per optimizer group'
+                if world > 1 else None,
+                'flop_per_step': sac_flop_per_step(B), 'measured': do_sac},
         'roofline': {'kernel': 'rollout_step_kernel', 'bound': 'mfma', 'achieved': achieved,
                      'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_PEAK_TFLOPS,
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,

@@ -34,6 +34,8 @@ class EnsembleEngine:
         self.ws = {}
         self.noise = None
         self.dev = model.group.data.device
+        from .distributed import GradReducer
+        self.dp = GradReducer()
 
     # ------------------------------------------------------------------ helpers
     def buf(self, name, *shape, dtype=torch.float32):
@@ -260,6 +262,7 @@ class EnsembleEngine:
             nets, strides, save_x = self._forward(xs, xa, b, E, b * S, b * A, tag='fit', save=True)
             _, gD, gL = self._loss(nets, xs, b * S, xt, b * S1, b, E, True, loss_out=losses[i], tag='fit')
             self._backward(nets, strides, save_x, gD, gL, b, E)
+            self.dp.mean_(m.group.grad)
             m.optimizer.step()
         # holdout: the same rows for every member (src/dynamics.py:175-183)
         hb = m.holdout_size
@@ -268,6 +271,7 @@ class EnsembleEngine:
         gather(hb, (hs, ha, ht))
         nets, _, _ = self._forward(hs, ha, hb, E, 0, 0, tag='ho')
         mse, _, _ = self._loss(nets, hs, 0, ht, 0, hb, E, False, tag='ho')
+        self.dp.mean_(mse)       # identical elites on every rank
         mse_h = mse.tolist()
         m.holdout_losses = mse_h
         m._elite_inds = [int(i) for i in np.argsort(np.asarray(mse_h, np.float32), kind='stable')[:m.num_elites]]
@@ -308,6 +312,7 @@ class EnsembleEngine:
                 ep_i = ep[bi:bi + 1].view(())
                 loss = self.compute_loss_value(xs, xa, xt, with_grads=True)
                 ep_i.copy_(loss)
+                self.dp.mean_(m.group.grad)
                 if max_grad_norm is not None:
                     part = grad_sumsq(m.group.grad)
                     sc = m.optimizer.step_scalars()

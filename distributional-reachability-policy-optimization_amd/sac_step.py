@@ -119,6 +119,8 @@ class SACEngine:
         self.sol = solver
         self.S, self.A, self.C = solver.state_dim, solver.action_dim, solver.con_dim
         self.dev = solver.actor.group.data.device
+        from .distributed import GradReducer
+        self.dp = GradReducer()
         from .envs import device_env_params
         self.env_params = device_env_params(solver.env) if solver.qc_under_uncertainty and \
             not solver.distributional_qc else None
@@ -349,6 +351,7 @@ class SACEngine:
             items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]]))
         self._run_wgrad('c.wg' + str(int(dist)), lambda: wgrad_items(items, B))
         cg = sol.critic_group
+        self.dp.mean_(cg.grad)
         crange = cg.span('critic.')
         ccrange = self._alive_span(cg, ['constraint_critic.trunk.', 'constraint_critic.mean_head.'] +
                                    (['constraint_critic.log_std_head.'] if dist else []))
@@ -455,13 +458,14 @@ class SACEngine:
         na, ns = n['actor'], n['safe']
         self._run_wgrad('a.wg', lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]]), (ns, [xs, ns.sy[0], ns.sy[1]])],
                                                     B))
+        ag = self.buf('a.alpha_grad', 1)
+        _lib.check(L.drpo_alpha_grad(sol.log_alpha.data_ptr(), asum.data_ptr(), B, ag.data_ptr(), _lib.stream()),
+                   'alpha_grad')
+        self.dp.mean_(sol.actor.group.grad, sol.actor_safe.group.grad, ag)
         # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam + cosine
         g = sol.actor.group
         self._clip_adam(sol.actor_optimizer, [(0, g.size)], g)
         sol.actor_lr_scheduler.step()
-        ag = self.buf('a.alpha_grad', 1)
-        _lib.check(L.drpo_alpha_grad(sol.log_alpha.data_ptr(), asum.data_ptr(), B, ag.data_ptr(), _lib.stream()),
-                   'alpha_grad')
         self._alpha_adam(ag)
         g = sol.actor_safe.group
         self._clip_adam(sol.actor_safe_optimizer, [(0, g.size)], g)
@@ -550,6 +554,7 @@ class SACEngine:
         nm = n['mult']
         self._run_bwd('m.bmult', lambda: fill_bwd([nm], [gx], B))
         self._run_wgrad('m.wg', lambda: wgrad_items([(nm, [xm, nm.sy[0], nm.sy[1]])], B))
+        self.dp.mean_(g.grad)
         self._clip_adam(sol.multiplier_optimizer, [(0, g.size)], g)
         sol.multiplier_lr_scheduler.step()
 

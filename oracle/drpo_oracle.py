@@ -559,7 +559,9 @@ class SSACOracle:
         P = self.P if P is None else P
         g, C = self.c['discount'], self.C
         with torch.no_grad():
-            a2, _, _, _ = policy_sample(P, 'actor_safe.net.', s2, rng)
+            robust = self.c['uncertainty'] and not self.c['distributional']
+            if not robust:
+                a2, _, _, _ = policy_sample(P, 'actor_safe.net.', s2, rng)
             dones = d.tile((C, 1)).t().squeeze().float()
             if self.c['uncertainty'] and self.c['distributional']:
                 _, _, q2 = cons_critic(P, 'constraint_critic_target.', s2, a2, 'sample', self.c['std_ratio'], rng)
@@ -569,7 +571,15 @@ class SSACOracle:
                 diff = torch.clamp(y - qm, min=-self.c['qc_td_bound'], max=self.c['qc_td_bound'])
                 return y, diff + qm
             if self.c['uncertainty']:
-                raise NotImplementedError('robust (model-sampled) certificate target is not restated')
+                # robust: s' from one elite member of the dynamics model, done from the
+                # env's check_done on it (src/ssac.py:387-400)
+                s2m, _ = ens_sample(P, 'model_ensemble.', s, a, self.c['elites'], rng)
+                dm, _, _ = env_fns(self.c['env'])(s2m)
+                a2m, _, _, _ = policy_sample(P, 'actor_safe.net.', s2m, rng)
+                q2 = cons_critic(P, 'constraint_critic_target.', s2m, a2m, 'mean')
+                dones = dm.tile((C, 1)).t().squeeze()
+                nonterm = (1. - g) * h + g * torch.maximum(h, q2)
+                return torch.where(dones, h, nonterm), None
             q2 = cons_critic(P, 'constraint_critic_target.', s2, a2, 'mean')
             nonterm = (1. - g) * h + g * torch.maximum(h, q2)
             return nonterm * (1 - dones.float()) + h * dones.float(), None

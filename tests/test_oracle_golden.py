@@ -126,12 +126,15 @@ def ssac_cfg(d):
                 actor_lr=1e-4, updates_per_training=1 * 2 * 10)
 
 
-@pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad'])
+@pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point'])
 def test_ssac_updates(tag):
     d = load_golden(f'ssac_{tag}')
     P0 = sd(d, 'sd0/')
     C, A = int(d['meta/C']), int(d['meta/A'])
-    orc = O.SSACOracle(P0, ssac_cfg(d), C, A)
+    cfg = ssac_cfg(d)
+    if 'model/elite_inds' in d.files:
+        cfg.update(elites=list(d['model/elite_inds']), env=str(d['meta/env']))
+    orc = O.SSACOracle(P0, cfg, C, A)
     batch = [torch.from_numpy(d['in/' + k]) for k in ['s', 'a', 's2', 'r', 'd', 'v', 'h']]
     rng = O.TapeRNG.from_npz(d, 'critic_tape')
     lq, lqc = orc.update_critic(*batch, rng)
