@@ -114,9 +114,67 @@ def wgrad_items(entries, rows):
     return arr, len(items)
 
 
+def fwd_flops(d):
+    """Algorithmic FLOPs of one drpo_mlp_forward launch (2 * rows * sum din*dout)."""
+    macs = 0
+    for j in range(d.nnets):
+        for l in range(d.net[j].nl):
+            macs += d.net[j].L[l].din * d.net[j].L[l].dout
+    return 2 * d.rows * d.nbatch * macs
+
+
+def bwd_flops(d):
+    """Backward-data products (dY = dZ W) of one drpo_mlp_backward launch; layer 0's
+    product is counted only when its input gradient is requested."""
+    macs = 0
+    for j in range(d.nnets):
+        n = d.net[j]
+        for l in range(n.nl):
+            if l > 0 or n.dx:
+                macs += n.L[l].din * n.L[l].dout
+    return 2 * d.rows * d.nbatch * macs
+
+
+def wgrad_flops(arr, n):
+    return sum(2 * arr[i].rows * arr[i].nbatch * arr[i].dout * (arr[i].din + 1) for i in range(n))
+
+
+class LaunchProfiler:
+    """HIP events around every MLP launch of the engine (stream-ordered on the launch
+    stream), with each launch's algorithmic FLOPs; summarise() after a synchronize."""
+
+    def __init__(self):
+        self.recs = []
+
+    def begin(self, kind, key, flops):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return (kind, key, flops, e0, e1)
+
+    def end(self, rec):
+        rec[4].record()
+        self.recs.append(rec)
+
+    def summarise(self):
+        out = {}
+        for kind, key, flops, e0, e1 in self.recs:
+            ms = e0.elapsed_time(e1)
+            for k in (kind, f'{kind}:{key}'):
+                o = out.setdefault(k, {'launches': 0, 'ms': 0.0, 'flop': 0.0})
+                o['launches'] += 1
+                o['ms'] += ms
+                o['flop'] += flops
+        for o in out.values():
+            o['avg_ms'] = o['ms'] / o['launches']
+            o['tflops'] = o['flop'] / (o['ms'] * 1e-3) / 1e12 if o['ms'] > 0 else 0.0
+        self.recs = []
+        return out
+
+
 class SACEngine:
     def __init__(self, solver):
         self.sol = solver
+        self.profiler = None
         self.S, self.A, self.C = solver.state_dim, solver.action_dim, solver.con_dim
         self.dev = solver.actor.group.data.device
         from .distributed import GradReducer
@@ -214,20 +272,29 @@ class SACEngine:
         d = self.desc.get(key)
         if d is None:
             d = self.desc[key] = builder()
+        ev = self.profiler.begin('mlp_fwd', key, fwd_flops(d)) if self.profiler else None
         _lib.check(_lib.lib().drpo_mlp_forward(ctypes.byref(d), _lib.stream()), key)
+        if ev:
+            self.profiler.end(ev)
 
     def _run_bwd(self, key, builder):
         d = self.desc.get(key)
         if d is None:
             d = self.desc[key] = builder()
+        ev = self.profiler.begin('mlp_bwd', key, bwd_flops(d)) if self.profiler else None
         _lib.check(_lib.lib().drpo_mlp_backward(ctypes.byref(d), _lib.stream()), key)
+        if ev:
+            self.profiler.end(ev)
 
     def _run_wgrad(self, key, builder):
         d = self.desc.get(key)
         if d is None:
             d = self.desc[key] = builder()
         arr, n = d
+        ev = self.profiler.begin('mlp_wgrad', key, wgrad_flops(arr, n)) if self.profiler else None
         _lib.check(_lib.lib().drpo_mlp_wgrad(arr, n, _lib.stream()), key)
+        if ev:
+            self.profiler.end(ev)
 
     def _policy_head(self, raw, mode, eps, site, ctr, a=None, logp=None, u=None, e=None, amean=None):
         L = _lib.lib()

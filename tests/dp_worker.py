@@ -44,6 +44,8 @@ def main():
     sd0 = solver_sd(d, 'sd0/')
     sol.log_alpha.fill_(float(sd0.pop('log_alpha')))
     sol.load_state_dict(sd0, strict=False)
+    if 'model/elite_inds' in d.files:
+        alg.model_ensemble._elite_inds = list(d['model/elite_inds'])
     if rank == 1:                       # diverge, then resync from rank 0
         sol.critic_group.data.add_(1.0)
     sync_parameters(alg)
