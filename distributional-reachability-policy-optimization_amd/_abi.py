@@ -28,6 +28,12 @@ class RolloutDesc(ctypes.Structure):
     ]
 
 
+class PackItem(ctypes.Structure):
+    """drpo_pack_item_t"""
+    _fields_ = [('W', P), ('P', P), ('PT', P), ('din', c_int), ('dout', c_int), ('nbatch', c_int),
+                ('wstride', c_int64), ('pstride', c_int64), ('ptstride', c_int64)]
+
+
 # name -> (restype, argtypes)
 PROTOTYPES = {
     'drpo_version': (c_int, []),
@@ -49,6 +55,8 @@ PROTOTYPES = {
     'drpo_normalizer_workspace_size': (c_size_t, [c_int64, c_int]),
     'drpo_normalizer_fit': (c_int, [P, c_int64, c_int, P, P, P, P]),
     'drpo_normalize': (c_int, [P, P, P, c_float, P, c_int64, c_int, P]),
+    'drpo_packed_size': (c_int64, [c_int, c_int]),
+    'drpo_pack_weights': (c_int, [POINTER(PackItem), c_int, P]),
     'drpo_ens_gather': (c_int, [P, P, P, P, c_int64, P, c_int64, c_int64, P, c_uint64, c_uint64, c_int, c_int, P, P,
                                 P, P]),
     'drpo_ens_head': (c_int, [P, P, P, c_int64, c_int64, c_int, c_int, P, P, P, P, c_uint64, c_uint64, P, P, P, P,

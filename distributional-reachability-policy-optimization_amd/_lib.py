@@ -9,7 +9,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libdrpo_hip.so')
+LIB_PATH = os.environ.get('DRPO_LIB_OVERRIDE') or os.path.join(_HERE, 'libdrpo_hip.so')   # override: profiling builds only
 _lib = None
 
 c_int, c_i64, c_u64, c_f32, c_sz, c_vp = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,

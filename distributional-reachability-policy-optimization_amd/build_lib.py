@@ -22,7 +22,12 @@ def _stale(src, obj, headers):
     return any(os.path.getmtime(p) > t for p in [src] + headers)
 
 
-def build(verbose=False, jobs=8):
+def build(verbose=False, jobs=8, variant=None):
+    """variant='stamps': profiling build with in-kernel s_memtime stamps (-DDRPO_STAMPS)
+    into libdrpo_hip_stamps.so; never loaded by the product."""
+    if variant == 'stamps':
+        return _build_variant(['-DDRPO_STAMPS'], os.path.join(HERE, 'libdrpo_hip_stamps.so'), 'build_stamps', verbose,
+                              jobs)
     os.makedirs(OBJ, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
     headers = glob.glob(os.path.join(CSRC, '*.hpp')) + glob.glob(os.path.join(HERE, '..', 'include', '*.h'))
@@ -49,5 +54,27 @@ def build(verbose=False, jobs=8):
     return LIB
 
 
+def _build_variant(defs, lib, objdir, verbose, jobs):
+    od = os.path.join(HERE, objdir)
+    os.makedirs(od, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    objs = [os.path.join(od, os.path.basename(s)[:-4] + '.o') for s in srcs]
+
+    def cc(so):
+        s, o = so
+        cmd = [HIPCC] + FLAGS + defs + ['-I', os.path.join(HERE, '..', 'include'), '-c', s, '-o', o]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed for {s}:\n{r.stderr}')
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(cc, zip(srcs, objs)))
+    r = subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', lib] + objs, capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'link failed:\n{r.stderr}')
+    return lib
+
+
 if __name__ == '__main__':
-    print(build(verbose='-v' in sys.argv))
+    print(build(verbose='-v' in sys.argv, variant='stamps' if '--stamps' in sys.argv else None))

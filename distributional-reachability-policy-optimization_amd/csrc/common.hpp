@@ -104,40 +104,28 @@ __device__ __forceinline__ void philox_normal4(uint64_t seed, uint32_t c0, uint3
 }
 
 // ---------------------------------------------------------------------------
-// tile_dense: out[r][c] = act(sum_k in[r][k] * W[c*ldw + k] + b[c]) for a tile of
-// RB*16 rows. `in` / `out` are LDS tiles with row strides ldi / ldo; columns
+// tile_dense: out[r][c] = act(sum_k in[r][k] * W[c][k] + b[c]) for a tile of RB*16
+// rows. `in` / `out` are LDS tiles with row strides ldi / ldo; columns
 // [N, round_up(N,16)) of `out` are written as 0 so the next layer can read a
-// zero-padded K. W is row-major [N][ldw] (PyTorch Linear layout) in global
-// memory (L2-resident: every workgroup streams the same weights).
+// zero-padded K.
 //
 // MFMA 16x16x4 f32 mapping (CDNA4): lane l supplies A[row=l&15][k=l>>4] and
 // B[k=l>>4][col=l&15]; D[row=4*(l>>4)+r][col=l&15] in acc[r]. A k-chunk of 16 is
 // fed as 4 MFMAs where lane group g=l>>4 supplies k = k0+4g+m for MFMA m, so
-// both operands are loaded as one float4 per lane (A: ds_read_b128 from LDS,
-// B: one 16-byte global load of 4 consecutive W[col][k]).
+// both operands are loaded as one float4 per lane (A: ds_read_b128 from LDS).
+//
+// Weights are read from a PACKED mirror (csrc/pack.hip, drpo_pack_weights): the
+// B fragment of (16-column block cb, 16-deep k-step s) is 256 contiguous floats,
+// lane l's float4 at offset 4*l, zero-padded beyond N and K:
+//     P[(cb*NKS + s)*256 + 4*l + i] = W[16*cb + (l&15)][16*s + 4*(l>>4) + i]
+// so every weight load is one lane-linear 1 KB wave access (8 full 128-B lines)
+// instead of 16 rows x 64 B (measured 2x slower per MFMA:
+// profiles/probes/load_probe.hip), and needs no clamping or masks. The
+// backward-data product (dY = dZ W) reads the transposed mirror of the same
+// shape with the roles of N and K exchanged.
 // ---------------------------------------------------------------------------
-template <int RB, int MAXC>
-struct DenseFrag {
-  f32x4 acc[RB][MAXC];
-};
-
-// Branch-free weight-fragment load. The address is clamped into the matrix and
-// NO mask is applied: k >= K lanes multiply zero-padded activation columns (every
-// LDS tile is zero beyond its width up to the next multiple of 16) and columns
-// j >= N are discarded by the epilogue, so the (finite) clamped values never reach
-// an output. With no control flow around the loads the compiler keeps several
-// k-steps in flight with counted vmcnt waits.
-template <bool VEC>
-__device__ __forceinline__ f32x4 load_w4(const float* __restrict__ W, int ldw, int j, int kk, int N, int K) {
-  const float* row = W + (size_t)(j < N ? j : N - 1) * ldw;
-  if constexpr (VEC) {   // K % 4 == 0, rows 16-byte aligned
-    return *reinterpret_cast<const f32x4*>(row + (kk < K ? kk : K - 4));
-  } else {
-    f32x4 r;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = row[kk + i < K ? kk + i : K - 1];
-    return r;
-  }
+__device__ __forceinline__ f32x4 load_pk(const float* __restrict__ P, int cb, int s, int NKS) {
+  return *reinterpret_cast<const f32x4*>(P + ((size_t)(cb * NKS + s) << 8) + ((threadIdx.x & 63) << 2));
 }
 
 // Weight fragments are streamed through a static register ring of depth PF_D:
@@ -184,30 +172,25 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
   }
 }
 
-// B fragment of the TRANSPOSED weight: lane (col n, group g) gets W[kk+i][n],
-// i = 0..3 (W row-major [K][ldw]); used by backward-data products dY = dZ * W.
-__device__ __forceinline__ f32x4 load_wT4(const float* __restrict__ W, int ldw, int n, int kk, int N, int K) {
-  const int nc = n < N ? n : N - 1;
-  f32x4 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = W[(size_t)(kk + i < K ? kk + i : K - 1) * ldw + nc];
-  return r;
-}
-
 // One layer for an RB*16-row tile by NW waves (NW*64 threads); wave w owns the
-// 16-column blocks w, w+NW, ... (MAXC of them).
+// 16-column blocks w, w+NW, ... (MAXC of them; blocks past N compute discarded
+// values from a clamped, valid fragment).
 // NK > 0: compile-time number of 16-deep k-steps -> fully unrolled, so the weight
 // ring and the one-step-ahead LDS A prefetch are indexed statically and the
 // compiler's vmcnt accounting never has to cross a loop back-edge (a back-edge
 // forces vmcnt(0), collapsing the prefetch distance). NK == 0: runtime K loop.
-template <int NW, int RB, int MAXC, int ACT, bool VEC, int NK, bool TRANS = false>
-__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
+template <int NW, int RB, int MAXC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,
                                                 const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
-#define DRPO_LOADB(col, kk) (TRANS ? load_wT4(W, ldw, (col), (kk), N, K) : load_w4<VEC>(W, ldw, (col), (kk), N, K))
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
+  const int NKS = NK > 0 ? NK : (K + 15) >> 4;
+  const int NCB = (N + 15) >> 4;
+  int cbs[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) cbs[c] = min(wave + NW * c, NCB - 1);
 
   f32x4 acc[RB][MAXC];
 #pragma unroll
@@ -219,8 +202,7 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
 #pragma unroll
   for (int u = 0; u < PF_D - 1; ++u)
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      bq[u][c] = DRPO_LOADB((wave + NW * c) * 16 + l15, 16 * u + 4 * g);
+    for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(P, cbs[c], min(u, NKS - 1), NKS);
 
   if constexpr (NK > 0) {
     f32x4 an[RB], ac[RB];
@@ -230,8 +212,7 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
     for (int s = 0; s < NK; ++s) {
       if (s + PF_D - 1 < NK) {
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c)
-          bq[(s + PF_D - 1) % PF_D][c] = DRPO_LOADB((wave + NW * c) * 16 + l15, 16 * (s + PF_D - 1) + 4 * g);
+        for (int c = 0; c < MAXC; ++c) bq[(s + PF_D - 1) % PF_D][c] = load_pk(P, cbs[c], s + PF_D - 1, NKS);
       }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
@@ -252,23 +233,22 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
             acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF_D][c][m], acc[rb][c], 0, 0, 0);
     }
   } else {
-    for (int kb = 0; kb < K; kb += 16 * PF_D) {
+    for (int kb = 0; kb < NKS; kb += PF_D) {
 #pragma unroll
       for (int u = 0; u < PF_D; ++u) {
-        const int k0 = kb + 16 * u;
-        const int kl = k0 + 16 * (PF_D - 1);
+        const int s = kb + u;
 #pragma unroll
         for (int c = 0; c < MAXC; ++c)
-          bq[(u + PF_D - 1) % PF_D][c] = DRPO_LOADB((wave + NW * c) * 16 + l15, kl + 4 * g);
-        if (k0 < K) {
+          bq[(u + PF_D - 1) % PF_D][c] = load_pk(P, cbs[c], min(s + PF_D - 1, NKS - 1), NKS);
+        if (s < NKS) {
           f32x4 a[RB];
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
-            a[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
+            a[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 16 * s + 4 * g);
 #pragma unroll
           for (int m = 0; m < 4; ++m)
 #pragma unroll
-            for (int c = 0; c < MAXC; ++c)   // out-of-range column blocks compute discarded values
+            for (int c = 0; c < MAXC; ++c)
 #pragma unroll
               for (int rb = 0; rb < RB; ++rb)
                 acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][m], bq[u][c][m], acc[rb][c], 0, 0, 0);
@@ -277,48 +257,29 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
     }
   }
   dense_epilogue<NW, RB, MAXC, ACT>(acc, bias, N, out, ldo, gs);
-#undef DRPO_LOADB
 }
 
-template <int NW, int RB, int MAXC, int ACT, bool VEC, bool TRANS = false>
-__device__ __forceinline__ void tile_dense_nk(const float* in, int ldi, int K, const float* W, int ldw,
-                                              const float* bias, int N, float* out, int ldo,
-                                              const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
-  switch ((K + 15) >> 4) {
-    case 1: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 1, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
-    case 13: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 13, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
-    case 16: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 16, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
-    default: tile_dense_impl<NW, RB, MAXC, ACT, VEC, 0, TRANS>(in, ldi, K, W, ldw, bias, N, out, ldo, gs); break;
-  }
-}
-
-// Row-aligned fast path (float4 weight loads) when K % 4 == 0, else scalar loads.
-// MAXC = column blocks per wave: ceil(ceil(N/16)/NW) must be <= MAXC.
+// K (input width) -> compile-time k-step count for the widths on the path
+// (14/13/12/11 inputs -> 1 step, 200 -> 13, 256 -> 16), else the runtime loop.
 template <int NW, int RB, int MAXC, int ACT>
-__device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
-                                           const float* __restrict__ bias, int N, float* out, int ldo,
-                                           const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
-  if ((ldw & 3) == 0 && (K & 3) == 0)
-    tile_dense_nk<NW, RB, MAXC, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo, gs);
-  else
-    tile_dense_nk<NW, RB, MAXC, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo, gs);
-}
-
-// out[r][n] = sum_k in[r][k] * W[k][n] (W row-major [K][ldw]): backward-data product.
-template <int NW, int RB, int MAXC>
-__device__ __forceinline__ void tile_dense_T(const float* in, int ldi, int K, const float* __restrict__ W, int ldw,
-                                             int N, float* out, int ldo) {
-  tile_dense_nk<NW, RB, MAXC, ACT_NONE, false, true>(in, ldi, K, W, ldw, nullptr, N, out, ldo);
+__device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, const float* P, const float* bias, int N,
+                                           float* out, int ldo, const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+  switch ((K + 15) >> 4) {
+    case 1: tile_dense_impl<NW, RB, MAXC, ACT, 1>(in, ldi, K, P, bias, N, out, ldo, gs); break;
+    case 13: tile_dense_impl<NW, RB, MAXC, ACT, 13>(in, ldi, K, P, bias, N, out, ldo, gs); break;
+    case 16: tile_dense_impl<NW, RB, MAXC, ACT, 16>(in, ldi, K, P, bias, N, out, ldo, gs); break;
+    default: tile_dense_impl<NW, RB, MAXC, ACT, 0>(in, ldi, K, P, bias, N, out, ldo, gs); break;
+  }
 }
 
 // Narrow layer (N <= 16, one column block): the K reduction is split over the NW
 // waves (k-steps s == wave mod NW), partial 16x16 tiles are summed through LDS
 // (`red`: NW*RB*256 floats), then bias + activation. Avoids one wave doing the
 // whole narrow head serially while the others idle.
-template <int NW, int RB, int ACT, bool VEC>
-__device__ __forceinline__ void tile_dense_narrow_impl(const float* in, int ldi, int K, const float* __restrict__ W,
-                                                       int ldw, const float* __restrict__ bias, int N, float* out,
-                                                       int ldo, float* red, const GSave& gs) {
+template <int NW, int RB, int ACT>
+__device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int K, const float* __restrict__ P,
+                                                  const float* __restrict__ bias, int N, float* out, int ldo,
+                                                  float* red, const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -332,18 +293,17 @@ __device__ __forceinline__ void tile_dense_narrow_impl(const float* in, int ldi,
 #pragma unroll
   for (int q = 0; q < MAXS; ++q) {
     const int s = wave + NW * q;
-    const int k0 = (s < NKS ? s : 0) * 16;
-    b[q] = load_w4<VEC>(W, ldw, l15, k0 + 4 * g, N, K);
+    const int sc = s < NKS ? s : 0;
+    b[q] = load_pk(P, 0, sc, NKS);
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
+    for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + sc * 16 + 4 * g);
   }
   for (int kb = NW * MAXS; kb < NKS; kb += NW) {   // K > 16*NW*MAXS (only for K > 256)
-    const int k0 = (kb + wave) * 16;
     if (kb + wave < NKS) {
-      const f32x4 bb = load_w4<VEC>(W, ldw, l15, k0 + 4 * g, N, K);
+      const f32x4 bb = load_pk(P, 0, kb + wave, NKS);
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
-        const f32x4 aa = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + k0 + 4 * g);
+        const f32x4 aa = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + (kb + wave) * 16 + 4 * g);
 #pragma unroll
         for (int m = 0; m < 4; ++m) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[m], bb[m], acc[rb], 0, 0, 0);
       }
@@ -378,16 +338,6 @@ __device__ __forceinline__ void tile_dense_narrow_impl(const float* in, int ldi,
       if (gs.gz) gs.gz[(size_t)row * gs.ldg + col] = z;
     }
   }
-}
-
-template <int NW, int RB, int ACT>
-__device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int K, const float* W, int ldw,
-                                                  const float* bias, int N, float* out, int ldo, float* red,
-                                                  const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
-  if ((ldw & 3) == 0 && (K & 3) == 0)
-    tile_dense_narrow_impl<NW, RB, ACT, true>(in, ldi, K, W, ldw, bias, N, out, ldo, red, gs);
-  else
-    tile_dense_narrow_impl<NW, RB, ACT, false>(in, ldi, K, W, ldw, bias, N, out, ldo, red, gs);
 }
 
 }  // namespace drpo

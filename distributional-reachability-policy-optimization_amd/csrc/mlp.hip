@@ -33,13 +33,33 @@ constexpr int MAXN = 3;
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
+#ifdef DRPO_STAMPS
+// profiling builds only (profiles/stamps.py): per-workgroup s_memtime stamps
+__device__ unsigned long long g_stamps[1 << 16][16];
+#define STAMP(i)                                                                                  \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long _t;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    const unsigned _w = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);          \
+    if (threadIdx.x == 0 && _w < (1u << 16)) g_stamps[_w][(i)] = _t;                              \
+  } while (0)
+DRPO_API int drpo_debug_stamps(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * (size_t)n);
+}
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 template <int ACT>
 __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const drpo_mlp_layer_t& L, const float* W,
                                               const float* b, float* out, int ldo, float* red, const GSave& gs) {
   if (L.dout <= 16)
-    tile_dense_narrow<FW_NW, 1, ACT>(in, ldi, L.din, W, L.din, b, L.dout, out, ldo, red, gs);
+    tile_dense_narrow<FW_NW, 1, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, red, gs);
   else
-    tile_dense<FW_NW, 1, FW_MAXC, ACT>(in, ldi, L.din, W, L.din, b, L.dout, out, ldo, gs);
+    tile_dense<FW_NW, 1, FW_MAXC, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, gs);
 }
 
 __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& L, int z, int64_t rows,
@@ -70,6 +90,7 @@ __device__ __forceinline__ float* run_net(const drpo_mlp_fwd_t& a, float* in, fl
       float* out = (cur == bufA) ? bufB : bufA;
       run_layer(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red);
       __syncthreads();
+      STAMP(2 + 4 * NI + l);
       cur = out;
     }
   }
@@ -90,6 +111,7 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
   const int nrows = (int)min((int64_t)FW_ROWS, a.rows - row0);
   const int din0 = a.cols[0] + a.cols[1] + a.cols[2];
   const int kpad = round_up(din0, 16);
+  STAMP(0);
 
   for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
     const int r = e / kpad, k = e - r * kpad;
@@ -114,6 +136,7 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
     xin[r * LDH + k] = v;
   }
   __syncthreads();
+  STAMP(1);
   if (!a.trunk) {
     if (blockIdx.y == 0) run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
     else if (blockIdx.y == 1) run_net<1>(a, xin, bA, bB, z, row0, nrows, red);
@@ -203,14 +226,15 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* 
     __syncthreads();
     float* out = (cur == bA) ? bB : bA;
     const float* W = L.W + (size_t)z * L.wstride;
-    tile_dense_T<FW_NW, 1, FW_MAXC>(cur, LDH, L.dout, W, L.din, L.din, out, LDH);
+    // dY_prev = dZ W: transposed mirror, N = din, K = dout
+    tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, L.dout, W, nullptr, L.din, out, LDH);
     __syncthreads();
     cur = out;
   }
   return cur;
 }
 
-__global__ __launch_bounds__(FW_NT) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* G = smem;
   float* bA = G + FW_ROWS * LDH;

@@ -200,11 +200,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   __syncthreads();
 
   // ---- 2. actor MLP (src/policy.py:61-100; mlp() ReLU hidden) ---------------
-  tile_dense<NW, RB, MAXC, ACT_RELU>(xin, p.ldx, S, p.aW1, S, p.ab1, p.Ha, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_RELU>(xin, p.ldx, S, p.aW1, p.ab1, p.Ha, h1, p.ldh);
   __syncthreads();
-  tile_dense<NW, RB, MAXC, ACT_RELU>(h1, p.ldh, p.Ha, p.aW2, p.Ha, p.ab2, p.Ha, h2, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_RELU>(h1, p.ldh, p.Ha, p.aW2, p.ab2, p.Ha, h2, p.ldh);
   __syncthreads();
-  tile_dense_narrow<NW, RB, ACT_NONE>(h2, p.ldh, p.Ha, p.aW3, p.Ha, p.ab3, 2 * A, ao, 20, red);
+  tile_dense_narrow<NW, RB, ACT_NONE>(h2, p.ldh, p.Ha, p.aW3, p.ab3, 2 * A, ao, 20, red);
   __syncthreads();
 
   // ---- 3. squashed Gaussian sample + model input [normalize(s), a] ----------
@@ -232,19 +232,19 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   __syncthreads();
 
   // ---- 4. elite member forward (src/dynamics.py:112-122, swish) -------------
-  tile_dense<NW, RB, MAXC, ACT_SILU>(xin, p.ldx, S + A, p.mW1, S + A, p.mb1, p.Hm, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(xin, p.ldx, S + A, p.mW1, p.mb1, p.Hm, h1, p.ldh);
   __syncthreads();
-  tile_dense<NW, RB, MAXC, ACT_SILU>(h1, p.ldh, p.Hm, p.mW2, p.Hm, p.mb2, p.Hm, h2, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(h1, p.ldh, p.Hm, p.mW2, p.mb2, p.Hm, h2, p.ldh);
   __syncthreads();
-  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.Hm, p.db1, p.Hm, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.db1, p.Hm, h1, p.ldh);
   __syncthreads();
-  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.Hm, p.db2, S1, dout, p.ldm, red);
-  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.Hm, p.db2, S1, dout, p.ldm);
+  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.ldm, red);
+  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.ldm);
   __syncthreads();
-  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.Hm, p.lb1, p.Hm, h1, p.ldh);
+  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.lb1, p.Hm, h1, p.ldh);
   __syncthreads();
-  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.Hm, p.lb2, S1, lout, p.ldm, red);
-  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.Hm, p.lb2, S1, lout, p.ldm);
+  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.lb2, S1, lout, p.ldm, red);
+  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.lb2, S1, lout, p.ldm);
   __syncthreads();
 
   // ---- 5. residual mean, log-var soft clamp, Gaussian sample ---------------
@@ -437,7 +437,8 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
     const float* Wm[6];
     const float* Bm[6];
     for (int i = 0; i < 6; ++i) {
-      Wm[i] = Wb[i] + (size_t)m * E_out_in[i][0] * E_out_in[i][1];
+      // packed mirrors: member stride = drpo_packed_size(in, out)
+      Wm[i] = Wb[i] + (size_t)m * drpo_packed_size(E_out_in[i][1], E_out_in[i][0]);
       Bm[i] = Bb[i] + (size_t)m * E_out_in[i][0];
     }
     a.mW1 = Wm[0]; a.mW2 = Wm[1]; a.dW1 = Wm[2]; a.dW2 = Wm[3]; a.lW1 = Wm[4]; a.lW2 = Wm[5];

@@ -77,3 +77,6 @@ def sync_parameters(alg, src=0):
     red.broadcast_(sol.actor.group.data, sol.actor_safe.group.data, sol.critic_group.data,
                    sol.critic_target_group.data, sol.multiplier.group.data, sol.log_alpha, m.group.data,
                    m.state_normalizer.mean, m.state_normalizer.std, src=src)
+    for g in (sol.actor.group, sol.actor_safe.group, sol.critic_group, sol.critic_target_group, sol.multiplier.group,
+              m.group):
+        g.mark_dirty()

@@ -74,6 +74,9 @@ class BatchedGaussianEnsemble(Configurable, Module):
         self.diff_spec.reference_init(g, 'diff_head.')
         self.logvar_spec.reference_init(g, 'log_var_head.')
         g.data, g.grad = g.data.to(device), g.grad.to(device)
+        from .params import spec_pack_layers
+        g.enable_packing(spec_pack_layers(self.trunk_spec, 'trunk.') + spec_pack_layers(self.diff_spec, 'diff_head.') +
+                         spec_pack_layers(self.logvar_spec, 'log_var_head.'))
         self.group = g
 
         self.min_log_var = nn.Parameter(g.view('min_log_var'), requires_grad=False)

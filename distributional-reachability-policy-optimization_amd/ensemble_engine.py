@@ -62,15 +62,17 @@ class EnsembleEngine:
         for prefix, spec in self._specs():
             lay, gl, st = [], [], []
             for i in range(spec.n_layers):
-                W, b = g.view(f'{prefix}{2 * i}.weight'), g.view(f'{prefix}{2 * i}.bias')
+                key = f'{prefix}{2 * i}.weight'
+                W, WT, b = g.pview(key), g.pview(key, True), g.view(f'{prefix}{2 * i}.bias')
                 din, dout = spec.dims[i], spec.dims[i + 1]
                 act = spec.act if i < spec.n_layers - 1 else spec.out_act
                 if member is not None:
-                    W, b = W[member], b[member]
+                    W, WT, b = W[member], WT[member], b[member]
                     st.append((0, 0))
-                else:
-                    st.append((dout * din, dout))
-                lay.append((W, b, din, dout, ACT_ID[act]))
+                else:          # packed-mirror stride per member, bias stride
+                    st.append((W.shape[1], dout))
+                    W, WT = W[0], WT[0]
+                lay.append((W, b, din, dout, ACT_ID[act], WT))
                 if grads:
                     gl.append((g.view(f'{prefix}{2 * i}.weight', g.grad), g.view(f'{prefix}{2 * i}.bias', g.grad)))
             nets.append(Net(lay, gl if grads else None))
@@ -84,11 +86,12 @@ class EnsembleEngine:
         m, L = self.m, _lib.lib()
         S, A = m.state_dim, m.action_dim
         S1 = S + 1
+        m.group.ensure_packed()
         nets, strides = self._nets(member, grads=save)
         rows = Z * n
         if save:
             for j, net in enumerate(nets):
-                for l, (_, _, din, dout, act) in enumerate(net.layers):
+                for l, (_, _, din, dout, act, _) in enumerate(net.layers):
                     net.sy[l] = self.buf(f'{tag}.sy{j}{l}', rows, dout)
                     net.sz[l] = self.buf(f'{tag}.sz{j}{l}', rows, dout) if act == ACT_ID['swish'] else None
                     net.dz[l] = self.buf(f'{tag}.dz{j}{l}', rows, dout)
@@ -201,7 +204,7 @@ class EnsembleEngine:
         trunk_out = nets[0].sy[-1]
         for j, net in enumerate(nets):
             ins = [save_x if j == 0 else trunk_out] + [net.sy[l] for l in range(len(net.layers) - 1)]
-            for l, (W, bb, din, dout, act) in enumerate(net.layers):
+            for l, (W, bb, din, dout, act, _) in enumerate(net.layers):
                 gW, gb = net.grad_layers[l]
                 it = WgradItem()
                 it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()

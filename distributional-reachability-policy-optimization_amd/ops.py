@@ -96,8 +96,18 @@ def rollout(alg, policy, initial_states, noise, timer=None):
 
     ws = alg._workspace('rollout', L.drpo_rollout_workspace_size(B, S, H))
     start_ptr = vb.pointer if vb._host_ptr is not None else None
-    actor = policy.layers()
-    trunk, diff, logv = model.views()
+    policy.group.ensure_packed()
+    model.group.ensure_packed()
+    pa = [(policy.group.pview(f'net.{2 * i}.weight')[0], policy.group.view(f'net.{2 * i}.bias'))
+          for i in range(policy.spec.n_layers)]
+    mg = model.group
+
+    def mviews(prefix, spec):   # packed mirrors of member 0 (the kernel adds member * packed size)
+        return [(mg.pview(f'{prefix}{2 * i}.weight')[0], mg.view(f'{prefix}{2 * i}.bias'))
+                for i in range(spec.n_layers)]
+    actor = pa
+    trunk, diff, logv = (mviews('trunk.', model.trunk_spec), mviews('diff_head.', model.diff_spec),
+                         mviews('log_var_head.', model.logvar_spec))
     ep = alg.env_params
     members_arr = (ctypes.c_int * H)(*members)
     d = RolloutDesc()
@@ -222,6 +232,7 @@ def _mlp(nets, srcs, rows, trunk=False, norm=None):
 
 def _net(group, prefix, spec, out_rows=None):
     from .sac_step import Net, spec_layers
+    group.ensure_packed()
     net = Net(spec_layers(group, prefix, spec))
     if out_rows is not None:
         net.sy[-1] = torch.empty(out_rows, net.dout, device=group.data.device)

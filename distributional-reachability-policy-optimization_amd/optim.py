@@ -63,6 +63,8 @@ class Adam:
                                _lib.ptr(self.v[start:end]), n, scalars[0], scalars[1], self.betas[0],
                                self.betas[1], self.eps, self.weight_decay, _lib.ptr(part), n_part,
                                float(max_norm), _lib.ptr(lr_scale), _lib.stream()), 'adam')
+        if self.group is not None:
+            self.group.mark_dirty()
 
     def step(self):
         """Plain step over the whole group (no clipping), for external training loops."""

@@ -55,11 +55,73 @@ class FlatGroup:
     def offset(self, name):
         return self.entries[name][0]
 
+    # ---- packed weight mirrors (csrc/pack.hip) ---------------------------------
+    def enable_packing(self, layers, transposed=None):
+        """layers: [(weight_name, din, dout, nbatch)]. Allocates the forward mirror
+        (and the transposed one for trained groups) that every MLP kernel streams."""
+        transposed = self.grad is not None if transposed is None else transposed
+        self.pk_layers = {}
+        off = 0
+        for name, din, dout, nb in layers:
+            sz = packed_size(din, dout)
+            self.pk_layers[name] = (off, sz, din, dout, nb)
+            off += sz * nb
+        dev = self.data.device
+        self.packed = torch.zeros(max(off, 64), dtype=torch.float32, device=dev)
+        self.packedT = torch.zeros(max(off, 64), dtype=torch.float32, device=dev) if transposed else None
+        self._pk_items = None
+        self._pk_ver = None
+        return self
+
+    def pview(self, name, transposed=False):
+        """[nbatch, packed_size] view of one layer's mirror (row z = member z)."""
+        off, sz, din, dout, nb = self.pk_layers[name]
+        buf = self.packedT if transposed else self.packed
+        return None if buf is None else buf[off:off + sz * nb].view(nb, sz)
+
+    def mark_dirty(self):
+        """The flat data was written by a kernel (Adam, EMA, a collective)."""
+        self._pk_ver = None
+
+    def ensure_packed(self):
+        """Refresh the mirrors if the weights changed (torch in-place writes bump the
+        shared version counter of the flat buffer and every view of it; kernel writes
+        call mark_dirty)."""
+        if getattr(self, 'pk_layers', None) is None or self._pk_ver == self.data._version:
+            return
+        from . import _lib
+        from ._abi import PackItem
+        if self._pk_items is None:
+            items = []
+            for name, (off, sz, din, dout, nb) in self.pk_layers.items():
+                it = PackItem()
+                it.W = self.view(name).data_ptr()
+                it.P = self.packed[off:].data_ptr()
+                it.PT = self.packedT[off:].data_ptr() if self.packedT is not None else 0
+                it.din, it.dout, it.nbatch = din, dout, nb
+                it.wstride, it.pstride, it.ptstride = din * dout, sz, sz
+                items.append(it)
+            self._pk_items = [(PackItem * len(items[i:i + 16]))(*items[i:i + 16]) for i in range(0, len(items), 16)]
+        L = _lib.lib()
+        for arr in self._pk_items:
+            _lib.check(L.drpo_pack_weights(arr, len(arr), _lib.stream()), f'pack {self.name}')
+        self._pk_ver = self.data._version
+
     def span(self, prefix):
         """(start, end) floats covering all entries whose name starts with prefix."""
         offs = [(self.entries[n][0], self.entries[n][0] + int(math.prod(self.entries[n][1])))
                 for n in self.order if n.startswith(prefix)]
         return min(o[0] for o in offs), max(o[1] for o in offs)
+
+
+def packed_size(din, dout):
+    """floats in one packed mirror of a [dout][din] weight (== drpo_packed_size)."""
+    return ((dout + 15) // 16) * ((din + 15) // 16) * 256
+
+
+def spec_pack_layers(spec, prefix):
+    """[(weight_name, din, dout, nbatch)] of an MLPSpec stored under prefix."""
+    return [(f'{prefix}{2 * i}.weight', spec.dims[i], spec.dims[i + 1], spec.E or 1) for i in range(spec.n_layers)]
 
 
 class LinearSlot(nn.Module):

@@ -47,6 +47,8 @@ class SquashedGaussianPolicy(Module):
             pol.spec.reference_init(g, 'net.')
         g.data = g.data.to(device)
         g.grad = g.grad.to(device)
+        from .params import spec_pack_layers
+        g.enable_packing(spec_pack_layers(pol.spec, 'net.'))
         pol.net = pol.spec.build(g, 'net.')
         return pol
 

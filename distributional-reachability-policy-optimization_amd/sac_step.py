@@ -28,14 +28,18 @@ SITE_PI_NEXT, SITE_SAFE_NEXT, SITE_PI_RS, SITE_SAFE_RS, SITE_PI_MULT = 1, 2, 5, 
 
 
 def spec_layers(group, prefix, spec, buf=None):
-    """[(W, b, din, dout, act)] for an MLPSpec stored under prefix in a flat group."""
+    """[(P, b, din, dout, act, PT)] for an MLPSpec stored under prefix in a flat group:
+    P / PT are the layer's packed forward / transposed weight mirrors (group.pview),
+    b the bias view (of ``buf`` if given, else the group data)."""
     out = []
     n = spec.n_layers
     for i in range(n):
         act = spec.act if i < n - 1 else spec.out_act
-        W = group.view(f'{prefix}{2 * i}.weight', buf)
+        key = f'{prefix}{2 * i}.weight'
         b = group.view(f'{prefix}{2 * i}.bias', buf)
-        out.append((W, b, spec.dims[i], spec.dims[i + 1], ACT_ID[act]))
+        PT = group.pview(key, True)
+        out.append((group.pview(key)[0], b, spec.dims[i], spec.dims[i + 1], ACT_ID[act],
+                    None if PT is None else PT[0]))
     return out
 
 
@@ -43,7 +47,7 @@ class Net:
     """One MLP as seen by the kernels: layer tuples + (optional) per-layer save buffers."""
 
     def __init__(self, layers, grad_layers=None):
-        self.layers = layers              # [(W, b, din, dout, act)]
+        self.layers = layers              # [(P, b, din, dout, act, PT)]
         self.grad_layers = grad_layers    # [(gW, gb)] or None
         self.sy = [None] * len(layers)
         self.sz = [None] * len(layers)
@@ -73,7 +77,7 @@ def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, ws
     d.save_x = _p(save_x)
     for j, net in enumerate(nets):
         d.net[j].nl = len(net.layers)
-        for l, (W, b, din, dout, act) in enumerate(net.layers):
+        for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
             L = d.net[j].L[l]
             L.W, L.b, L.din, L.dout, L.act = W.data_ptr(), b.data_ptr(), din, dout, act
             L.sy, L.sz = _p(net.sy[l]), _p(net.sz[l])
@@ -87,9 +91,10 @@ def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None):
     d = MlpBwd()
     for j, net in enumerate(nets):
         d.net[j].nl = len(net.layers)
-        for l, (W, b, din, dout, act) in enumerate(net.layers):
+        for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
             L = d.net[j].L[l]
-            L.W, L.din, L.dout, L.act = W.data_ptr(), din, dout, act
+            assert WT is not None, 'backward needs the transposed weight mirror (trained group)'
+            L.W, L.din, L.dout, L.act = WT.data_ptr(), din, dout, act
             L.sy, L.sz, L.dz = _p(net.sy[l]), _p(net.sz[l]), _p(net.dz[l])
             L.wstride = 0 if wstride is None else wstride[j][l][0]
         d.net[j].gout = _p(gouts[j])
@@ -104,7 +109,7 @@ def wgrad_items(entries, rows):
     """entries: [(net, inputs_per_layer)] -> ctypes array of WgradItem."""
     items = []
     for net, ins in entries:
-        for l, (W, b, din, dout, act) in enumerate(net.layers):
+        for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
             gW, gb = net.grad_layers[l]
             it = WgradItem()
             it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
@@ -241,7 +246,7 @@ class SACEngine:
         for key, net in n.items():
             if net.grad_layers is None:
                 continue
-            for l, (_, _, din, dout, act) in enumerate(net.layers):
+            for l, (_, _, din, dout, act, _) in enumerate(net.layers):
                 net.sy[l] = buf(f'{key}.sy{l}', B, dout)
                 net.dz[l] = buf(f'{key}.dz{l}', B, dout)
         for key in ('q0t', 'q1t', 'cc_trunkt', 'cc_meant', 'cc_lst'):
@@ -268,6 +273,13 @@ class SACEngine:
         return t
 
     # ------------------------------------------------------------------ helpers
+    def _ensure_packed(self):
+        """Refresh the packed weight mirrors of every group an update step reads."""
+        sol = self.sol
+        for g in (sol.actor.group, sol.actor_safe.group, sol.critic_group, sol.critic_target_group,
+                  sol.multiplier.group):
+            g.ensure_packed()
+
     def _run_fwd(self, key, builder):
         d = self.desc.get(key)
         if d is None:
@@ -338,6 +350,7 @@ class SACEngine:
 
     def _critic_step(self, noise):
         sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        self._ensure_packed()
         self.noise = noise = noise or self.noise
         L = _lib.lib()
         dist = sol.distributional_qc and sol.qc_under_uncertainty
@@ -428,6 +441,7 @@ class SACEngine:
             sol.critic_optimizer.apply(cg.grad, s0, s1, sc, clip=(part, sol.grad_norm))
         sol.critic_lr_scheduler.step()
         ema_(sol.critic_target_group.data, cg.data, sol.tau)
+        sol.critic_target_group.mark_dirty()
         return loss[0], loss[1]
 
     def _out_net(self, net, name, B):
@@ -446,6 +460,7 @@ class SACEngine:
 
     def _actor_step(self, noise):
         sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        self._ensure_packed()
         self.noise = noise = noise or self.noise
         L = _lib.lib()
         ws = self.ws
@@ -550,7 +565,7 @@ class SACEngine:
         v = self.nets_view.get(name)
         if v is None:
             v = Net(net.layers, net.grad_layers)
-            for l, (_, _, din, dout, act) in enumerate(net.layers):
+            for l, (_, _, din, dout, act, _) in enumerate(net.layers):
                 v.sy[l] = self.buf(f'{name}.sy{l}', self.B, dout)
             self.nets_view[name] = v
         return v
@@ -582,6 +597,7 @@ class SACEngine:
 
     def _mult_step(self, noise):
         sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        self._ensure_packed()
         self.noise = noise = noise or self.noise
         L = _lib.lib()
         ws = self.ws

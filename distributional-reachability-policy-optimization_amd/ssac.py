@@ -204,6 +204,13 @@ class SSAC(Module):
         tg = FlatGroup('critic_target')
         tg.entries, tg.order, tg.size = dict(cg.entries), list(cg.order), cg.size
         tg.data, tg.grad = cg.data.clone(), None
+        from .params import spec_pack_layers
+        crit_layers = [x for i in range(critic.n_critics) for x in spec_pack_layers(critic.spec, f'critic.qs.{i}.')]
+        crit_layers += (spec_pack_layers(cc.trunk_spec, 'constraint_critic.trunk.') +
+                        spec_pack_layers(cc.mean_spec, 'constraint_critic.mean_head.') +
+                        spec_pack_layers(cc.logstd_spec, 'constraint_critic.log_std_head.'))
+        cg.enable_packing(crit_layers)
+        tg.enable_packing(crit_layers, transposed=False)
         critic.build(cg, 'critic.')
         cc.build(cg, 'constraint_critic.')
         critic_t = CriticEnsemble(self.critic_cfg, state_dim, action_dim, prefix='critic.')
@@ -225,6 +232,7 @@ class SSAC(Module):
         mg.allocate('cpu')
         mult.spec.reference_init(mg, 'lam.')
         mg.data, mg.grad = mg.data.to(device), mg.grad.to(device)
+        mg.enable_packing(spec_pack_layers(mult.spec, 'lam.'))
         mult.lam = mult.spec.build(mg, 'lam.')
         mult.group = mg
         self.multiplier = mult

@@ -57,8 +57,8 @@ typedef struct {
   int S, A, C, Ha, Hm, B, H;
   int env_id, tracking_surr_start, tracking_n_surr;
   float quad_x_threshold, quad_z_threshold;
-  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;          /* actor Linear layers [out][in] */
-  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2; /* ensemble [E][out][in] */
+  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;          /* actor: packed weight mirrors + biases */
+  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2; /* ensemble: packed mirrors [E] (member stride drpo_packed_size) + biases [E][out] */
   const float *norm_mean, *norm_std, *min_lv, *max_lv;
   const int* members;            /* host [H]: elite member per step (random.choice, src/dynamics.py:199) */
   const float* replay_states;    /* real buffer states, physical layout */
@@ -97,12 +97,12 @@ int drpo_sample_without_replacement(int64_t* out, int64_t B, int64_t N, uint64_t
  * nbatch = ensemble members). Used by the SAC update (src/ssac.py:437-578),
  * the ensemble fit (src/dynamics.py:143-187) and every network forward.      */
 typedef struct {
-  const float* W; /* [dout][din] */
+  const float* W; /* packed forward mirror of the [dout][din] weight (drpo_pack_weights) */
   const float* b; /* [dout] */
   int din, dout, act;
   float* sy;      /* optional: post-activation save [rows][dout] */
   float* sz;      /* optional: pre-activation save */
-  int64_t wstride, bstride; /* per batch item (ensemble member) */
+  int64_t wstride, bstride; /* per batch item (ensemble member): packed-mirror / bias strides */
 } drpo_mlp_layer_t;
 
 typedef struct {
@@ -126,7 +126,7 @@ typedef struct {
 } drpo_mlp_fwd_t;
 
 typedef struct {
-  const float* W;
+  const float* W;      /* packed TRANSPOSED mirror of the [dout][din] weight */
   int din, dout, act;
   const float* sy;
   const float* sz;
@@ -164,6 +164,21 @@ typedef struct {
 int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);
 int drpo_mlp_backward(const drpo_mlp_bwd_t* desc /* host */, drpo_stream_t stream);
 int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, drpo_stream_t stream);
+
+/* ---------------------------------------------------------------- packed weight mirrors
+ * Every MLP kernel streams weights from fragment-linear mirrors of the PyTorch
+ * [nbatch][dout][din] tensors (layout: csrc/pack.hip). The mirrors are refreshed
+ * by one drpo_pack_weights launch per parameter group after it changes.        */
+typedef struct {
+  const float* W;     /* [nbatch][dout][din], member stride wstride */
+  float* P;           /* forward mirror (or NULL), member stride pstride */
+  float* PT;          /* transposed (backward-data) mirror (or NULL), stride ptstride */
+  int din, dout, nbatch;
+  int64_t wstride, pstride, ptstride;
+} drpo_pack_item_t;
+
+int64_t drpo_packed_size(int din, int dout); /* floats per mirror of one [dout][din] matrix */
+int drpo_pack_weights(const drpo_pack_item_t* items /* host, <= 16 */, int n, drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- SAC heads
  * (src/ssac.py:284-578, src/smbpo.py:251-279, src/policy.py:89-97)            */

@@ -1,0 +1,57 @@
+"""In-kernel phase timing of mlp_fwd_kernel (profiling build with s_memtime stamps).
+Runs with DRPO_LIB_OVERRIDE=<...>/libdrpo_hip_stamps.so. For each case prints the
+per-workgroup cycles spent in each phase (input staging, each layer) and the
+spread of workgroup start / end times across the grid."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench
+    import drpo_amd
+    from drpo_amd import _lib, ops
+    L = _lib.lib()
+    L.drpo_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device('cuda')
+    alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON)
+    sol = alg.solver
+    s = torch.randn(4096, 12, device=dev)
+    a = torch.rand(4096, 2, device=dev) * 2 - 1
+    cases = {
+        'actor 12-256-256-4': lambda: ops.policy_raw(sol.actor, s),
+        'twin critic 14-256-256-1 x2': lambda: sol.critic.all(s, a),
+        'cc trunk+2 heads': lambda: sol.constraint_critic(s, a, uncertainty=True),
+    }
+    buf = np.zeros((1 << 16, 16), np.uint64)
+    for name, fn in cases.items():
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        L.drpo_debug_stamps(ctypes.c_void_p(0), 0)
+        fn()
+        torch.cuda.synchronize()
+        L.drpo_debug_stamps(buf.ctypes.data, 1 << 16)
+        st = buf.astype(np.int64)
+        nwg = int((st[:, 0] > 0).sum())
+        st = st[:nwg]
+        t0 = st[:, 0]
+        print(f'== {name}: {nwg} workgroups')
+        print(f'   start spread {t0.max() - t0.min()} cyc; total span {st.max() - t0.min()} cyc')
+        cols = [c for c in range(1, 16) if (st[:, c] > 0).all()]
+        prev = 0
+        for c in cols:
+            d = st[:, c] - st[:, prev]
+            print(f'   phase {prev}->{c}: mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
+            prev = c
+        buf[:] = 0
+
+
+if __name__ == '__main__':
+    main()
