@@ -313,11 +313,23 @@ DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, drpo_stream_t stream_) {
 // ---------------------------------------------------------------------------
 // grouped weight gradients
 // ---------------------------------------------------------------------------
+// dW[o][i] = sum_r dZ[r][o] * Y[r][i], db[o] = sum_r dZ[r][o] for every layer of a
+// parameter group in ONE launch (tile table over items). A workgroup owns a 64x64
+// (o, i) tile and a 1024-row chunk; 64-row stages of dZ and Y are copied into
+// LDS in their natural row-major layout (coalesced 16-byte loads, conflict-free
+// 16-byte LDS writes). Each wave takes 16 rows of a stage: one ds_read_b128 of
+// 4 consecutive o and one of 4 consecutive i per row give 4x4 = 16 MFMAs
+// (MFMA m covers o = o0+4*lane15+m, MFMA n covers i = i0+4*lane15+n, k = row),
+// so the operands need no transposition. The 4 waves' partial tiles are summed
+// through LDS and added to the flat gradient with one float atomic per element
+// (row chunks of the same tile accumulate through the atomics; caller zeroes).
+// The bias gradient is a column sum of the staged dZ (i-tile 0 only).
 namespace {
-constexpr int WG_TILE = 64;
+constexpr int WG_T = 64;            // o x i tile
+constexpr int WG_STAGE = 64;        // rows per LDS stage
 constexpr int WG_CHUNK = 1024;      // rows per workgroup (split-K over the batch)
 constexpr int WG_MAXITEMS = 16;
-constexpr int WG_LDK = 16 + 4;      // LDS [col][k] row stride
+constexpr int WG_LD = 64 + 4;       // LDS row stride (floats)
 }  // namespace
 
 struct WgradArgs {
@@ -326,16 +338,30 @@ struct WgradArgs {
   int n;
 };
 
+// rows [r, r+1) x 64 columns [c0, c0+64) of a row-major [rows][ld] matrix -> 16 floats
+// per thread quarter; out-of-range entries are 0
+__device__ __forceinline__ f32x4 wg_load4(const float* __restrict__ M, int64_t r, int64_t r1, int c, int ncols,
+                                          bool vec) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (r >= r1) return v;
+  const float* row = M + r * ncols;
+  if (vec && c + 3 < ncols) return *reinterpret_cast<const f32x4*>(row + c);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) v[u] = (c + u < ncols) ? row[c + u] : 0.f;
+  return v;
+}
+
 __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) float As[2][WG_TILE * WG_LDK];   // dz^T  [o][k]
-  __shared__ __attribute__((aligned(16))) float Bs[2][WG_TILE * WG_LDK];   // y^T   [i][k]
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  float* Az = wsm;                                // [2][STAGE][LD]  dZ stage
+  float* By = wsm + 2 * WG_STAGE * WG_LD;         // [2][STAGE][LD]  Y stage
   const int64_t bid = blockIdx.x;
   int q = 0;
   while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
   const drpo_wgrad_item_t& I = a.it[q];
   int64_t loc = bid - a.first[q];
-  const int ti = (I.din + 1 + WG_TILE - 1) / WG_TILE;      // +1: bias ("ones") column
-  const int to = (I.dout + WG_TILE - 1) / WG_TILE;
+  const int ti = (I.din + WG_T - 1) / WG_T;
+  const int to = (I.dout + WG_T - 1) / WG_T;
   const int nch = (int)((I.rows + WG_CHUNK - 1) / WG_CHUNK);
   const int ch = (int)(loc % nch); loc /= nch;
   const int it_i = (int)(loc % ti); loc /= ti;
@@ -343,81 +369,107 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
   const int zb = (int)loc;
   const float* dz = I.dz + (size_t)zb * I.zstride;
   const float* y = I.y + (size_t)zb * I.ystride;
-  const int o0 = it_o * WG_TILE, i0 = it_i * WG_TILE;
+  const int o0 = it_o * WG_T, i0 = it_i * WG_T;
   const int64_t r0 = (int64_t)ch * WG_CHUNK;
   const int64_t r1 = min(I.rows, r0 + WG_CHUNK);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
-  // staging: thread -> (k = tid >> 4, col4 = (tid & 15) * 4)
-  const int sk = tid >> 4, sc = (tid & 15) * 4;
-  float ra[4], rbv[4];
-  auto gload = [&](int64_t rbase) {
-    const int64_t r = rbase + sk;
-    const bool rok = r < r1;
+  const bool vz = (I.dout & 3) == 0 && ((uintptr_t)dz & 15) == 0;
+  const bool vy = (I.din & 3) == 0 && ((uintptr_t)y & 15) == 0;
+  const bool do_bias = it_i == 0;
+  // staging map: thread -> rows (tid>>4) + 16*j, columns 4*(tid&15)
+  const int sr = tid >> 4, sc = 4 * (tid & 15);
+  f32x4 pz[4], py[4];
+  auto gload = [&](int64_t rb) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int o = o0 + sc + u, i = i0 + sc + u;
-      ra[u] = (rok && o < I.dout) ? dz[r * I.dout + o] : 0.f;
-      rbv[u] = (!rok || i > I.din) ? 0.f : (i == I.din ? 1.f : y[r * I.din + i]);
+    for (int j = 0; j < 4; ++j) {
+      pz[j] = wg_load4(dz, rb + sr + 16 * j, r1, o0 + sc, I.dout, vz);
+      py[j] = wg_load4(y, rb + sr + 16 * j, r1, i0 + sc, I.din, vy);
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      As[buf][(sc + u) * WG_LDK + sk] = ra[u];
-      Bs[buf][(sc + u) * WG_LDK + sk] = rbv[u];
+    for (int j = 0; j < 4; ++j) {
+      *reinterpret_cast<f32x4*>(&Az[(buf * WG_STAGE + sr + 16 * j) * WG_LD + sc]) = pz[j];
+      *reinterpret_cast<f32x4*>(&By[(buf * WG_STAGE + sr + 16 * j) * WG_LD + sc]) = py[j];
     }
   };
-  f32x4 acc[2][2];
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int w = 0; w < 2; ++w) acc[x][w] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int ob = (wave >> 1) * 2, ib = (wave & 1) * 2;   // 16-blocks handled by this wave
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;          // bias partial: column (tid & 63), rows (tid >> 6) + 4k of each stage
   gload(r0);
   sstore(0);
   __syncthreads();
   int buf = 0;
-  for (int64_t rb = r0; rb < r1; rb += 16) {
-    const bool more = rb + 16 < r1;
-    if (more) gload(rb + 16);
-    f32x4 fa[2], fb[2];
+  for (int64_t rb = r0; rb < r1; rb += WG_STAGE) {
+    const bool more = rb + WG_STAGE < r1;
+    if (more) gload(rb + WG_STAGE);
+    const float* A = Az + buf * WG_STAGE * WG_LD;
+    const float* Bm = By + buf * WG_STAGE * WG_LD;
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      fa[x] = *reinterpret_cast<const f32x4*>(&As[buf][((ob + x) * 16 + l15) * WG_LDK + 4 * g]);
-      fb[x] = *reinterpret_cast<const f32x4*>(&Bs[buf][((ib + x) * 16 + l15) * WG_LDK + 4 * g]);
+    for (int kg = 0; kg < 4; ++kg) {
+      const int r = 16 * wave + 4 * kg + g;
+      const f32x4 av = *reinterpret_cast<const f32x4*>(&A[r * WG_LD + 4 * l15]);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(&Bm[r * WG_LD + 4 * l15]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
     }
+    if (do_bias) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int w = 0; w < 2; ++w)
-          acc[x][w] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[x][m], fb[w][m], acc[x][w], 0, 0, 0);
+      for (int k = 0; k < WG_STAGE / 4; ++k) bsum += A[((tid >> 6) + 4 * k) * WG_LD + (tid & 63)];
+    }
     if (more) {
       sstore(buf ^ 1);
       __syncthreads();
       buf ^= 1;
     }
   }
-  float* gW = I.gW + (size_t)zb * I.gwstride;
-  float* gb = I.gb + (size_t)zb * I.gbstride;
+  __syncthreads();
+  // reduce the 4 waves' partial tiles: red[o_local][i_local] (64 x 64), waves add in turn
+  float* red = wsm;                               // 64 * 65 floats (reuses the stages)
+  constexpr int RL = 65;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
-      const int i = i0 + (ib + w) * 16 + l15;
+      for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = o0 + (ob + x) * 16 + 4 * g + r;
-        if (o >= I.dout || i > I.din) continue;
-        const float v = acc[x][w][r];
-        if (i < I.din) atomicAdd(&gW[(size_t)o * I.din + i], v);
-        else atomicAdd(&gb[o], v);
-      }
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int ol = 4 * (4 * g + rr) + m, il = 4 * l15 + n;
+            float* p = &red[ol * RL + il];
+            *p = (w == 0 ? 0.f : *p) + acc[m][n][rr];
+          }
     }
+    __syncthreads();
+  }
+  float* gW = I.gW + (size_t)zb * I.gwstride;
+  for (int e = tid; e < WG_T * WG_T; e += 256) {
+    const int ol = e >> 6, il = e & 63;
+    const int o = o0 + ol, i = i0 + il;
+    if (o < I.dout && i < I.din) atomicAdd(&gW[(size_t)o * I.din + i], red[ol * RL + il]);
+  }
+  if (do_bias) {
+    __syncthreads();
+    float* bred = wsm + WG_T * RL;
+    bred[tid] = bsum;
+    __syncthreads();
+    if (tid < 64) {
+      const float v = bred[tid] + bred[tid + 64] + bred[tid + 128] + bred[tid + 192];
+      const int o = o0 + tid;
+      if (o < I.dout) atomicAdd(&I.gb[(size_t)zb * I.gbstride + o], v);
+    }
+  }
 }
+
+static size_t wgrad_lds() { return sizeof(float) * (size_t)4 * WG_STAGE * WG_LD; }
 
 DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
@@ -432,14 +484,14 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t
     if (I.rows == 0) continue;
     a.it[m] = I;
     a.first[m] = tot;
-    const int64_t ti = (I.din + 1 + WG_TILE - 1) / WG_TILE, to = (I.dout + WG_TILE - 1) / WG_TILE;
+    const int64_t ti = (I.din + WG_T - 1) / WG_T, to = (I.dout + WG_T - 1) / WG_T;
     tot += ti * to * ((I.rows + WG_CHUNK - 1) / WG_CHUNK) * I.nbatch;
     ++m;
   }
   a.first[m] = tot;
   a.n = m;
   if (tot == 0) return DRPO_OK;
-  mlp_wgrad_kernel<<<(unsigned)tot, 256, 0, stream>>>(a);
+  mlp_wgrad_kernel<<<(unsigned)tot, 256, wgrad_lds(), stream>>>(a);
   DRPO_LAUNCH_CHECK("mlp_wgrad");
   return DRPO_OK;
 }
