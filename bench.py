@@ -191,42 +191,46 @@ def main():
         except (ImportError, NotImplementedError):
             do_sac = False
 
-    timer = EventTimer(2 * H)
     roll_ms, sac_ms, kern_ms, step_ms, n_trans = [], [], [], [], 0
 
-    def one_step(timed):
-        nonlocal n_trans
+    n_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def one_step(tmr):
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
         t2 = torch.cuda.Event(enable_timing=True)
         t0.record()
-        out = alg.rollout(alg.actor, timer=timer if timed else None)
+        out = alg.rollout(alg.actor, timer=tmr)
         t1.record()
         if do_sac:
             for st in range(alg.solver_updates_per_step):
                 alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
         t2.record()
-        return out, (t0, t1, t2)
+        n_dev.add_(out._count)            # device-side transition count (no host sync)
+        return (t0, t1, t2)
 
     for _ in range(args.warmup):
-        one_step(False)
+        one_step(None)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    n_dev.zero_()
+    # no host synchronisation inside the timed region: the host enqueues ahead of the
+    # GPU, so the per-phase event intervals are GPU time, not host launch latency
+    timers = [EventTimer(2 * H) for _ in range(args.steps)]
     wall0 = time.perf_counter()
-    for _ in range(args.steps):
-        out, evs = one_step(True)
-        torch.cuda.synchronize()         # per-step sync only to read the step's events
-        roll_ms.append(evs[0].elapsed_time(evs[1]))
-        sac_ms.append(evs[1].elapsed_time(evs[2]))
-        kern_ms.extend(timer.elapsed_pairs(H))
-        n_trans += len(out)
+    evs = [one_step(timers[i]) for i in range(args.steps)]
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - wall0
+    for e, tmr in zip(evs, timers):
+        roll_ms.append(e[0].elapsed_time(e[1]))
+        sac_ms.append(e[1].elapsed_time(e[2]))
+        kern_ms.extend(tmr.elapsed_pairs(H))
+    n_trans = int(n_dev.item())
     tot = torch.tensor([wall, sum(roll_ms) / 1e3, sum(sac_ms) / 1e3, float(n_trans)], dtype=torch.float64, device=dev)
     if dist is not None:
         mx = tot.clone()

@@ -34,6 +34,21 @@ class PackItem(ctypes.Structure):
                 ('wstride', c_int64), ('pstride', c_int64), ('ptstride', c_int64)]
 
 
+class PackMap(ctypes.Structure):
+    """drpo_pack_map_t (lives in device memory)"""
+    _fields_ = [('nlayers', c_int), ('off', c_int64 * 16), ('din', c_int * 16), ('dout', c_int * 16),
+                ('nbatch', c_int * 16), ('poff', c_int64 * 16), ('P', P), ('PT', P), ('Pt', P)]
+
+
+class OptimSeg(ctypes.Structure):
+    """drpo_optim_seg_t"""
+    _fields_ = [('p', P), ('g', P), ('m', P), ('v', P), ('start', c_int64), ('end', c_int64), ('adam', c_int),
+                ('partial', P), ('n_partial', c_int), ('max_norm', c_float),
+                ('lr_over_bc1', c_float), ('bc2_sqrt', c_float), ('beta1', c_float), ('beta2', c_float),
+                ('eps', c_float), ('weight_decay', c_float), ('zero_grad', c_int),
+                ('ema_target', P), ('ema_rate', c_float), ('ema_keep', c_float), ('map', P)]
+
+
 # name -> (restype, argtypes)
 PROTOTYPES = {
     'drpo_version': (c_int, []),
@@ -56,6 +71,8 @@ PROTOTYPES = {
     'drpo_normalizer_fit': (c_int, [P, c_int64, c_int, P, P, P, P]),
     'drpo_normalize': (c_int, [P, P, P, c_float, P, c_int64, c_int, P]),
     'drpo_packed_size': (c_int64, [c_int, c_int]),
+    'drpo_optim_step': (c_int, [POINTER(OptimSeg), c_int, P]),
+    'drpo_grad_sumsq_multi': (c_int, [POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), c_int, P]),
     'drpo_pack_weights': (c_int, [POINTER(PackItem), c_int, P]),
     'drpo_ens_gather': (c_int, [P, P, P, P, c_int64, P, c_int64, c_int64, P, c_uint64, c_uint64, c_int, c_int, P, P,
                                 P, P]),

@@ -203,7 +203,7 @@ __device__ __forceinline__ float act_grad(int act, float y, float z) {
 
 // G (LDS, width of the net output) -> gradient w.r.t. the net input (returned LDS buffer)
 __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* G, float* bA, float* bB, int z, int64_t rows,
-                          int row0, int nrows) {
+                          int row0, int nrows, bool need_dx0) {
   const int tid = threadIdx.x;
   float* cur = G;
   for (int l = net.nl - 1; l >= 0; --l) {
@@ -224,6 +224,7 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* 
       cur[r * LDH + k] = g;
     }
     __syncthreads();
+    if (l == 0 && !need_dx0) return nullptr;   // input gradient not wanted: dZ_0 (saved) is all wgrad needs
     float* out = (cur == bA) ? bB : bA;
     const float* W = L.W + (size_t)z * L.wstride;
     // dY_prev = dZ W: transposed mirror, N = din, K = dout
@@ -268,8 +269,8 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   if (!a.trunk) {
     const drpo_mlp_bwd_net_t& n = a.net[blockIdx.y];
     load_gout(n, G);
-    const float* gx = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows);
-    store_dx(n, gx);
+    const float* gx = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, n.dx != nullptr);
+    if (gx) store_dx(n, gx);
     return;
   }
   const int tw = a.net[0].L[a.net[0].nl - 1].dout;
@@ -278,15 +279,15 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __syncthreads();
   for (int h = 1; h < a.nnets; ++h) {
     load_gout(a.net[h], G);
-    const float* gh = bwd_net(a.net[h], G, bA, bB, z, a.rows, row0, nrows);
+    const float* gh = bwd_net(a.net[h], G, bA, bB, z, a.rows, row0, nrows, true);
     for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) {
       const int r = e / twpad, k = e - r * twpad;
       DT[r * LDH + k] += gh[r * LDH + k];
     }
     __syncthreads();
   }
-  const float* gx = bwd_net(a.net[0], DT, bA, bB, z, a.rows, row0, nrows);
-  store_dx(a.net[0], gx);
+  const float* gx = bwd_net(a.net[0], DT, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
+  if (gx) store_dx(a.net[0], gx);
 }
 
 static size_t bwd_lds() { return sizeof(float) * (size_t)4 * FW_ROWS * LDH; }

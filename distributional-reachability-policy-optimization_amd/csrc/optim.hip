@@ -208,3 +208,166 @@ DRPO_API int drpo_normalize(const float* x, const float* mean, const float* std,
   DRPO_LAUNCH_CHECK("normalize");
   return DRPO_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Fused optimizer step over segments of flat groups (one launch per SAC update
+// phase): clip coefficient from precomputed partial sums, Adam, gradient zeroing
+// for the next backward, EMA of a target group, and the refresh of the packed
+// weight mirrors the MLP kernels stream (so no separate zero / EMA / pack
+// launches). Elements are processed independently; segments never overlap.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int OPT_MAXSEG = 8;
+constexpr int OPT_BLOCK_ELEMS = 1024;   // elements per workgroup (256 threads x 4)
+}
+
+struct OptimArgs {
+  drpo_optim_seg_t seg[OPT_MAXSEG];
+  int64_t first[OPT_MAXSEG + 1];        // block prefix per segment
+  int n;
+};
+
+__device__ __forceinline__ void pack_write(const drpo_pack_map_t* mp, int64_t i, float pv, float tv, bool has_t) {
+  // find the weight matrix containing flat index i (<= 16 entries, uniform per block mostly)
+  for (int l = 0; l < mp->nlayers; ++l) {
+    const int din = mp->din[l], dout = mp->dout[l];
+    const int msz = din * dout;                       // group tensors are < 2^31 floats
+    const int64_t rel64 = i - mp->off[l];
+    if (rel64 < 0 || rel64 >= (int64_t)msz * mp->nbatch[l]) continue;
+    const int rel = (int)rel64;
+    const int z = rel / msz;
+    const int w = rel - z * msz;
+    const int o = w / din, k = w - o * din;
+    const int ncb = (dout + 15) >> 4, nks = (din + 15) >> 4;
+    const int64_t base = mp->poff[l] + (int64_t)z * ncb * nks * 256;
+    // forward mirror: fragment (o>>4, k>>4), lane ((k>>2)&3)*16 + (o&15), component k&3
+    const int64_t pi = base + ((int64_t)((o >> 4) * nks + (k >> 4)) << 8) + ((((k >> 2) & 3) * 16 + (o & 15)) << 2) + (k & 3);
+    if (mp->P) mp->P[pi] = pv;
+    if (has_t && mp->Pt) mp->Pt[pi] = tv;
+    if (mp->PT) {   // transposed mirror: fragment (k>>4, o>>4), lane ((o>>2)&3)*16 + (k&15), component o&3
+      const int64_t ti = base + ((int64_t)((k >> 4) * ncb + (o >> 4)) << 8) + ((((o >> 2) & 3) * 16 + (k & 15)) << 2) + (o & 3);
+      mp->PT[ti] = pv;
+    }
+    return;
+  }
+}
+
+__global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
+  __shared__ float s_coef;
+  const int64_t bid = blockIdx.x;
+  int q = 0;
+  while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
+  const drpo_optim_seg_t& S = a.seg[q];
+  if (S.partial) {
+    if (threadIdx.x < 64) {
+      float s = 0.f;
+      for (int i = threadIdx.x; i < S.n_partial; i += 64) s += S.partial[i];
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+      if (threadIdx.x == 0) {
+        const float c = S.max_norm / (sqrtf(s) + 1e-6f);
+        s_coef = c < 1.f ? c : 1.f;
+      }
+    }
+    __syncthreads();
+  }
+  const float coef = S.partial ? s_coef : 1.f;
+  const int64_t e0 = S.start + (bid - a.first[q]) * OPT_BLOCK_ELEMS;
+  const int64_t e1 = min(S.end, e0 + OPT_BLOCK_ELEMS);
+  for (int64_t i = e0 + threadIdx.x; i < e1; i += 256) {
+    float p = S.p[i];
+    if (S.adam) {
+      float g = S.g[i] * coef;
+      if (S.weight_decay != 0.f) g = fmaf(p, S.weight_decay, g);
+      const float m = torch_lerp(S.m[i], g, 1.f - S.beta1);
+      const float v = fmaf(S.v[i], S.beta2, (1.f - S.beta2) * g * g);
+      S.m[i] = m;
+      S.v[i] = v;
+      const float denom = sqrtf(v) / S.bc2_sqrt + S.eps;
+      p = p - S.lr_over_bc1 * (m / denom);
+      S.p[i] = p;
+    }
+    if (S.zero_grad) S.g[i] = 0.f;
+    float t = 0.f;
+    if (S.ema_target) {
+      t = S.ema_rate * p + S.ema_keep * S.ema_target[i];
+      S.ema_target[i] = t;
+    }
+    if (S.map) pack_write(S.map, i, p, t, S.ema_target != nullptr);
+  }
+}
+
+DRPO_API int drpo_optim_step(const drpo_optim_seg_t* segs, int n, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(n >= 0 && n <= OPT_MAXSEG, "drpo_optim_step: at most %d segments", OPT_MAXSEG);
+  OptimArgs a{};
+  int64_t tot = 0;
+  for (int k = 0; k < n; ++k) {
+    const drpo_optim_seg_t& S = segs[k];
+    DRPO_REQUIRE(S.p && S.end >= S.start && (!S.adam || (S.g && S.m && S.v)), "drpo_optim_step: bad segment %d", k);
+    a.seg[k] = S;
+    a.first[k] = tot;
+    tot += (S.end - S.start + OPT_BLOCK_ELEMS - 1) / OPT_BLOCK_ELEMS;
+  }
+  a.first[n] = tot;
+  a.n = n;
+  if (tot == 0) return DRPO_OK;
+  optim_step_kernel<<<(unsigned)tot, 256, 0, stream>>>(a);
+  DRPO_LAUNCH_CHECK("optim_step");
+  return DRPO_OK;
+}
+
+// partial sums of squares for several clip segments in one launch:
+// segment k writes drpo_grad_sumsq_blocks(end-start) partials at out[k]
+namespace {
+constexpr int SQ_MAXSEG = 8;
+}
+struct SumsqArgs {
+  const float* g[SQ_MAXSEG];
+  int64_t n[SQ_MAXSEG];
+  float* out[SQ_MAXSEG];
+  int64_t first[SQ_MAXSEG + 1];
+  int cnt;
+};
+
+__global__ __launch_bounds__(256) void sumsq_multi_kernel(SumsqArgs a) {
+  __shared__ float red[256];
+  const int64_t bid = blockIdx.x;
+  int q = 0;
+  while (q + 1 < a.cnt && bid >= a.first[q + 1]) ++q;
+  const int64_t lb = bid - a.first[q];
+  const int64_t base = lb * SUMSQ_BLOCK_ELEMS;
+  const float* g = a.g[q];
+  float s = 0.f;
+  for (int64_t i = base + threadIdx.x; i < min(a.n[q], base + (int64_t)SUMSQ_BLOCK_ELEMS); i += 256) {
+    const float v = g[i];
+    s = fmaf(v, v, s);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.out[q][lb] = red[0];
+}
+
+DRPO_API int drpo_grad_sumsq_multi(const float* const* g, const int64_t* n, float* const* out, int cnt,
+                                   drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(cnt >= 0 && cnt <= SQ_MAXSEG, "drpo_grad_sumsq_multi: at most %d segments", SQ_MAXSEG);
+  SumsqArgs a{};
+  int64_t tot = 0;
+  for (int k = 0; k < cnt; ++k) {
+    a.g[k] = g[k];
+    a.n[k] = n[k];
+    a.out[k] = out[k];
+    a.first[k] = tot;
+    tot += drpo_grad_sumsq_blocks(n[k]);
+  }
+  a.first[cnt] = tot;
+  a.cnt = cnt;
+  if (tot == 0) return DRPO_OK;
+  sumsq_multi_kernel<<<(unsigned)tot, 256, 0, stream>>>(a);
+  DRPO_LAUNCH_CHECK("grad_sumsq_multi");
+  return DRPO_OK;
+}

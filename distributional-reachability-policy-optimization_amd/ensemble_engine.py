@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .optim import fused_step
 from .rng import DeviceNoise
 from .sac_step import ACT_ID, Net, fill_bwd, fill_fwd
 from ._abi import WgradItem
@@ -259,14 +260,17 @@ class EnsembleEngine:
                                          _lib.ptr(idx_t), nz.seed, ctr, S, A, _lib.ptr(out[0]), _lib.ptr(out[1]),
                                          _lib.ptr(out[2]), _lib.stream()), 'ens_gather')
 
+        g = m.group
+        g.grad.zero_()
         for i in range(steps):
             gather(rows, (xs, xa, xt))
-            m.group.grad.zero_()
             nets, strides, save_x = self._forward(xs, xa, b, E, b * S, b * A, tag='fit', save=True)
             _, gD, gL = self._loss(nets, xs, b * S, xt, b * S1, b, E, True, loss_out=losses[i], tag='fit')
             self._backward(nets, strides, save_x, gD, gL, b, E)
-            self.dp.mean_(m.group.grad)
-            m.optimizer.step()
+            self.dp.mean_(g.grad)
+            # Adam + grad zeroing + packed-mirror refresh in one launch
+            fused_step([m.optimizer.segment(0, g.size, m.optimizer.step_scalars(), zero_grad=True,
+                                            pack_map=g.pack_map())])
         # holdout: the same rows for every member (src/dynamics.py:175-183)
         hb = m.holdout_size
         assert hb == b, 'reference asserts holdout_size == batch_size (src/dynamics.py:177)'

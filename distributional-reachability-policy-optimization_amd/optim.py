@@ -66,6 +66,28 @@ class Adam:
         if self.group is not None:
             self.group.mark_dirty()
 
+    def segment(self, start, end, scalars, clip=None, zero_grad=False, ema=None, pack_map=None, grad=None):
+        """drpo_optim_seg_t for elements [start, end) of this optimizer's tensor:
+        clip = (partials, max_norm); ema = (target flat tensor, rate); pack_map = device
+        drpo_pack_map_t of the group (refreshes its packed mirrors)."""
+        from ._abi import OptimSeg
+        self._ensure_state()
+        d = self._data()
+        g = grad if grad is not None else (self.group.grad if self.group is not None else self.tensor.grad)
+        sg = OptimSeg()
+        sg.p, sg.g, sg.m, sg.v = d.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr()
+        sg.start, sg.end, sg.adam = start, end, 1
+        if clip is not None:
+            sg.partial, sg.n_partial, sg.max_norm = clip[0].data_ptr(), clip[0].numel(), float(clip[1])
+        sg.lr_over_bc1, sg.bc2_sqrt = scalars
+        sg.beta1, sg.beta2 = self.betas
+        sg.eps, sg.weight_decay = self.eps, self.weight_decay
+        sg.zero_grad = int(zero_grad)
+        if ema is not None:
+            sg.ema_target, sg.ema_rate, sg.ema_keep = ema[0].data_ptr(), float(ema[1]), float(1.0 - float(ema[1]))
+        sg.map = 0 if pack_map is None else pack_map.data_ptr()
+        return sg
+
     def step(self):
         """Plain step over the whole group (no clipping), for external training loops."""
         sc = self.step_scalars()
@@ -122,3 +144,32 @@ def ema_(target, source, rate):
     L = _lib.lib()
     _lib.require_device(target, source)
     _lib.check(L.drpo_ema(_lib.ptr(target), _lib.ptr(source), target.numel(), float(rate), _lib.stream()), 'ema')
+
+
+def ema_segment(p, start, end, target, rate, pack_map=None):
+    """EMA-only segment (parameters not stepped by Adam, e.g. the vanilla log-std head)."""
+    from ._abi import OptimSeg
+    sg = OptimSeg()
+    sg.p, sg.start, sg.end, sg.adam = p.data_ptr(), start, end, 0
+    sg.ema_target, sg.ema_rate, sg.ema_keep = target.data_ptr(), float(rate), float(1.0 - float(rate))
+    sg.map = 0 if pack_map is None else pack_map.data_ptr()
+    return sg
+
+
+def fused_step(segs):
+    """One drpo_optim_step launch over the given segments."""
+    from ._abi import OptimSeg
+    L = _lib.lib()
+    arr = (OptimSeg * len(segs))(*segs)
+    _lib.check(L.drpo_optim_step(arr, len(segs), _lib.stream()), 'optim_step')
+
+
+def grad_sumsq_multi(slices, outs):
+    """Partial sums of squares of several gradient slices in one launch."""
+    import ctypes
+    L = _lib.lib()
+    n = len(slices)
+    g = (ctypes.c_void_p * n)(*[t.data_ptr() for t in slices])
+    cnt = (ctypes.c_int64 * n)(*[t.numel() for t in slices])
+    o = (ctypes.c_void_p * n)(*[t.data_ptr() for t in outs])
+    _lib.check(L.drpo_grad_sumsq_multi(g, cnt, o, n, _lib.stream()), 'grad_sumsq_multi')

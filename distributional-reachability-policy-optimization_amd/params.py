@@ -79,6 +79,30 @@ class FlatGroup:
         buf = self.packedT if transposed else self.packed
         return None if buf is None else buf[off:off + sz * nb].view(nb, sz)
 
+    def pack_map(self, target=None):
+        """Device-resident drpo_pack_map_t of this group's weight matrices (for the
+        fused optimizer step); ``target``: a group of identical layout whose forward
+        mirror is refreshed from the EMA'd values."""
+        key = None if target is None else target.name
+        cache = self.__dict__.setdefault('_pk_maps', {})
+        if key in cache:
+            return cache[key]
+        from ._abi import PackMap
+        import ctypes
+        mp = PackMap()
+        mp.nlayers = len(self.pk_layers)
+        assert mp.nlayers <= 16
+        for j, (name, (off, sz, din, dout, nb)) in enumerate(self.pk_layers.items()):
+            mp.off[j] = self.entries[name][0]
+            mp.din[j], mp.dout[j], mp.nbatch[j], mp.poff[j] = din, dout, nb, off
+        mp.P = self.packed.data_ptr()
+        mp.PT = self.packedT.data_ptr() if self.packedT is not None else 0
+        mp.Pt = target.packed.data_ptr() if target is not None else 0
+        raw = bytes(mp)
+        dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.data.device)
+        cache[key] = dev
+        return dev
+
     def mark_dirty(self):
         """The flat data was written by a kernel (Adam, EMA, a collective)."""
         self._pk_ver = None

@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 from ._abi import (BufferView, CriticHead, MlpBwd, MlpFwd, WgradItem)
-from .optim import grad_sumsq, ema_
+from .optim import ema_segment, fused_step, grad_sumsq_multi
 
 ACT_ID = {None: 0, 'identity': 0, 'relu': 1, 'swish': 2, 'tanh': 3}
 
@@ -130,12 +130,13 @@ def fwd_flops(d):
 
 def bwd_flops(d):
     """Backward-data products (dY = dZ W) of one drpo_mlp_backward launch; layer 0's
-    product is counted only when its input gradient is requested."""
+    product runs only for trunk-mode heads (it feeds the trunk) or when the input
+    gradient is requested."""
     macs = 0
     for j in range(d.nnets):
         n = d.net[j]
         for l in range(n.nl):
-            if l > 0 or n.dx:
+            if l > 0 or n.dx or (d.trunk and j > 0):
                 macs += n.L[l].din * n.L[l].dout
     return 2 * d.rows * d.nbatch * macs
 
@@ -191,6 +192,7 @@ class SACEngine:
         self.ws = {}
         self.loss_pool = None
         self.loss_pos = 0
+        self._zeroed = set()   # groups whose grads the last fused step left zeroed
         self.noise = None
 
     # ------------------------------------------------------------------ buffers
@@ -320,13 +322,15 @@ class SACEngine:
                                            float(cc.log_std_min), float(cc.log_std_max), ubmax.data_ptr(), None,
                                            _lib.stream()), 'cc_head')
 
-    def _clip_adam(self, opt, ranges, group, lr_scale=None):
-        """clip_grad_norm_ over each range separately (its own norm), then one Adam step
-        (shared step count / lr) over the ranges."""
-        sc = opt.step_scalars()
-        for (s0, s1) in ranges:
-            part = grad_sumsq(group.grad[s0:s1], self.buf(f'part.{group.name}.{s0}', 4096))
-            opt.apply(group.grad, s0, s1, sc, clip=(part, self.sol.grad_norm))
+    def _clean_grads(self, group):
+        """Gradients must be zero before the backward passes accumulate into them; the
+        fused optimizer step leaves them zeroed, so this only clears after anything else."""
+        if group.name not in self._zeroed:
+            group.grad.zero_()
+        self._zeroed.discard(group.name)
+
+    def _grads_zeroed(self, group):
+        self._zeroed.add(group.name)
 
     def _alive_span(self, group, prefixes):
         spans = [group.span(p) for p in prefixes]
@@ -397,7 +401,7 @@ class SACEngine:
         self._run_fwd('c.cc', lambda: fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B,
                                                trunk=True))
         loss = self._loss_slots(2)
-        sol.critic_group.grad.zero_()
+        self._clean_grads(sol.critic_group)
         ch = self.desc.get('c.head')
         if ch is None:
             ch = self.desc['c.head'] = CriticHead()
@@ -435,13 +439,25 @@ class SACEngine:
         crange = cg.span('critic.')
         ccrange = self._alive_span(cg, ['constraint_critic.trunk.', 'constraint_critic.mean_head.'] +
                                    (['constraint_critic.log_std_head.'] if dist else []))
+        # two clip norms (critic, constraint critic), one Adam step, grad zeroing, EMA of
+        # the whole target group and the packed-mirror refresh: 2 launches
+        tg = sol.critic_target_group
+        parts = [self.buf(f'part.c.{s0}', 4096)[:_lib.lib().drpo_grad_sumsq_blocks(s1 - s0)] for s0, s1 in
+                 (crange, ccrange)]
+        grad_sumsq_multi([cg.grad[s0:s1] for s0, s1 in (crange, ccrange)], parts)
         sc = sol.critic_optimizer.step_scalars()
-        for (s0, s1) in (crange, ccrange):
-            part = grad_sumsq(cg.grad[s0:s1], self.buf(f'part.c.{s0}', 4096))
-            sol.critic_optimizer.apply(cg.grad, s0, s1, sc, clip=(part, sol.grad_norm))
+        mp = cg.pack_map(tg)
+        segs = [sol.critic_optimizer.segment(s0, s1, sc, clip=(pt, sol.grad_norm), zero_grad=True,
+                                             ema=(tg.data, sol.tau), pack_map=mp)
+                for (s0, s1), pt in zip((crange, ccrange), parts)]
+        lo = 0
+        for s0, s1 in sorted((crange, ccrange)) + [(cg.size, cg.size)]:
+            if s0 > lo:      # parameters without a gradient (vanilla log-std head): EMA only
+                segs.append(ema_segment(cg.data, lo, s0, tg.data, sol.tau, mp))
+            lo = max(lo, s1)
+        fused_step(segs)
+        self._grads_zeroed(cg)
         sol.critic_lr_scheduler.step()
-        ema_(sol.critic_target_group.data, cg.data, sol.tau)
-        sol.critic_target_group.mark_dirty()
         return loss[0], loss[1]
 
     def _out_net(self, net, name, B):
@@ -533,8 +549,8 @@ class SACEngine:
         _lib.check(L.drpo_squash_backward(B, A, raws.data_ptr(), u_s.data_ptr(), e_s.data_ptr(), dAs.data_ptr(),
                                           None, 0.0, None, 0.0, None, draws.data_ptr(), _lib.stream()),
                    'squash_backward_safe')
-        sol.actor.group.grad.zero_()
-        sol.actor_safe.group.grad.zero_()
+        self._clean_grads(sol.actor.group)
+        self._clean_grads(sol.actor_safe.group)
         self._run_bwd('a.bact', lambda: fill_bwd([n['actor']], [draw], B))
         self._run_bwd('a.bsafe', lambda: fill_bwd([n['safe']], [draws], B))
         na, ns = n['actor'], n['safe']
@@ -544,13 +560,25 @@ class SACEngine:
         _lib.check(L.drpo_alpha_grad(sol.log_alpha.data_ptr(), asum.data_ptr(), B, ag.data_ptr(), _lib.stream()),
                    'alpha_grad')
         self.dp.mean_(sol.actor.group.grad, sol.actor_safe.group.grad, ag)
-        # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam + cosine
-        g = sol.actor.group
-        self._clip_adam(sol.actor_optimizer, [(0, g.size)], g)
+        # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam +
+        # cosine -- one sum-of-squares launch and one fused optimizer launch
+        ga, gs = sol.actor.group, sol.actor_safe.group
+        L = _lib.lib()
+        pa = self.buf('part.a', 4096)[:L.drpo_grad_sumsq_blocks(ga.size)]
+        ps = self.buf('part.s', 4096)[:L.drpo_grad_sumsq_blocks(gs.size)]
+        grad_sumsq_multi([ga.grad, gs.grad], [pa, ps])
+        aopt = sol.alpha_optimizer
+        if aopt.tensor is None:
+            aopt.tensor = sol.log_alpha.view(1)
+        segs = [sol.actor_optimizer.segment(0, ga.size, sol.actor_optimizer.step_scalars(), clip=(pa, sol.grad_norm),
+                                            zero_grad=True, pack_map=ga.pack_map()),
+                aopt.segment(0, 1, aopt.step_scalars(), grad=ag),
+                sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
+                                                 clip=(ps, sol.grad_norm), zero_grad=True, pack_map=gs.pack_map())]
+        fused_step(segs)
+        self._grads_zeroed(ga)
+        self._grads_zeroed(gs)
         sol.actor_lr_scheduler.step()
-        self._alpha_adam(ag)
-        g = sol.actor_safe.group
-        self._clip_adam(sol.actor_safe_optimizer, [(0, g.size)], g)
         sol.actor_safe_lr_scheduler.step()
 
     def _alpha_adam(self, grad):
@@ -633,12 +661,17 @@ class SACEngine:
                                           float(sol.penalty_ub), float(mc.upper_bound), float(sol.lam_epsilon),
                                           gx.data_ptr(), None, _lib.stream()), 'multiplier_head')
         g = sol.multiplier.group
-        g.grad.zero_()
+        self._clean_grads(g)
         nm = n['mult']
         self._run_bwd('m.bmult', lambda: fill_bwd([nm], [gx], B))
         self._run_wgrad('m.wg', lambda: wgrad_items([(nm, [xm, nm.sy[0], nm.sy[1]])], B))
         self.dp.mean_(g.grad)
-        self._clip_adam(sol.multiplier_optimizer, [(0, g.size)], g)
+        pm = self.buf('part.m', 4096)[:_lib.lib().drpo_grad_sumsq_blocks(g.size)]
+        grad_sumsq_multi([g.grad], [pm])
+        fused_step([sol.multiplier_optimizer.segment(0, g.size, sol.multiplier_optimizer.step_scalars(),
+                                                     clip=(pm, sol.grad_norm), zero_grad=True,
+                                                     pack_map=g.pack_map())])
+        self._grads_zeroed(g)
         sol.multiplier_lr_scheduler.step()
 
     # ------------------------------------------------------------------

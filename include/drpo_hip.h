@@ -285,6 +285,36 @@ int drpo_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr_
               const float* lr_scale, drpo_stream_t stream);
 int drpo_ema(float* target, const float* source, int64_t n, float rate, drpo_stream_t stream);
 
+/* Fused optimizer step over segments of flat groups: clip coefficient from the
+ * partial sums (clip_grad_norm_, src/ssac.py:450-451), Adam (src/defaults.py:4),
+ * gradient zeroing, EMA of a target group (src/torch_util.py:223-226) and the
+ * packed-mirror refresh, in ONE launch.                                        */
+typedef struct {              /* device memory: where each weight matrix of a group lives */
+  int nlayers;
+  int64_t off[16];            /* flat offset of the [nbatch][dout][din] weight */
+  int din[16], dout[16], nbatch[16];
+  int64_t poff[16];           /* offset of its packed mirrors (forward / transposed / target) */
+  float *P, *PT, *Pt;         /* mirrors (PT, Pt may be NULL) */
+} drpo_pack_map_t;
+
+typedef struct {
+  float *p, *g, *m, *v;       /* flat group (element indices are absolute) */
+  int64_t start, end;
+  int adam;                   /* 0: no Adam update (EMA / pack only) */
+  const float* partial;       /* clip partial sums (drpo_grad_sumsq[_multi]) or NULL */
+  int n_partial;
+  float max_norm;
+  float lr_over_bc1, bc2_sqrt, beta1, beta2, eps, weight_decay;
+  int zero_grad;              /* write g = 0 after use */
+  float* ema_target;          /* optional: target = rate*p + keep*target */
+  float ema_rate, ema_keep;
+  const drpo_pack_map_t* map; /* optional (device): packed mirrors to refresh */
+} drpo_optim_seg_t;
+
+int drpo_optim_step(const drpo_optim_seg_t* segs /* host, <= 8 */, int n, drpo_stream_t stream);
+int drpo_grad_sumsq_multi(const float* const* g /* host arrays */, const int64_t* n, float* const* partial_out, int cnt,
+                          drpo_stream_t stream);
+
 /* Normalizer.fit / forward (src/normalization.py:14-23) */
 size_t drpo_normalizer_workspace_size(int64_t N, int S);
 int drpo_normalizer_fit(const float* X, int64_t N, int S, float* mean, float* std, void* workspace,
