@@ -96,11 +96,12 @@ __device__ __forceinline__ void philox_normal4(uint64_t seed, uint32_t c0, uint3
                                                uint32_t c3, float out[4]) {
   u32x4 r = philox({c0, c1, c2, c3}, (uint32_t)seed, (uint32_t)(seed >> 32));
   float u1 = u32_to_unit(r.x), u2 = u32_to_unit(r.y), u3 = u32_to_unit(r.z), u4 = u32_to_unit(r.w);
-  float m1 = sqrtf(-2.f * logf(u1)), m2 = sqrtf(-2.f * logf(u3));
-  float s1, c1f, s2, c2f;
-  sincosf(6.28318530718f * u2, &s1, &c1f);
-  sincosf(6.28318530718f * u4, &s2, &c2f);
-  out[0] = m1 * c1f; out[1] = m1 * s1; out[2] = m2 * c2f; out[3] = m2 * s2;
+  // Box-Muller on the hardware transcendentals: v_log_f32 is log2, v_sin/v_cos take
+  // the angle in turns (sin(2*pi*x)), so no range reduction is needed for u in (0,1]
+  const float m1 = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(u1));
+  const float m2 = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(u3));
+  out[0] = m1 * __builtin_amdgcn_cosf(u2); out[1] = m1 * __builtin_amdgcn_sinf(u2);
+  out[2] = m2 * __builtin_amdgcn_cosf(u4); out[3] = m2 * __builtin_amdgcn_sinf(u4);
 }
 
 // ---------------------------------------------------------------------------
@@ -144,8 +145,21 @@ struct GSave {
   int nrows;
 };
 
+// bias values of this lane's output columns, loaded before the k-loop so their
+// latency hides behind it (loaded after the loop they cost a full L2 round trip
+// per layer)
+template <int NW, int MAXC>
+__device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N, float (&bv)[MAXC]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int col = (wave + NW * c) * 16 + (lane & 15);
+    bv[c] = (bias && col < N) ? bias[col] : 0.f;
+  }
+}
+
 template <int NW, int RB, int MAXC, int ACT>
-__device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], const float* __restrict__ bias, int N,
+__device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], const float (&bvs)[MAXC], int N,
                                                float* out, int ldo, const GSave& gs) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -155,7 +169,7 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
     const int cb = wave + NW * c;
     if (cb >= NB) continue;
     const int col = cb * 16 + l15;
-    const float bv = (col < N && bias) ? bias[col] : 0.f;
+    const float bv = bvs[c];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -203,6 +217,8 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
   for (int u = 0; u < PF_D - 1; ++u)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(P, cbs[c], min(u, NKS - 1), NKS);
+  float bvs[MAXC];
+  load_bias<NW, MAXC>(bias, N, bvs);
 
   if constexpr (NK > 0) {
     f32x4 an[RB], ac[RB];
@@ -256,7 +272,7 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
       }
     }
   }
-  dense_epilogue<NW, RB, MAXC, ACT>(acc, bias, N, out, ldo, gs);
+  dense_epilogue<NW, RB, MAXC, ACT>(acc, bvs, N, out, ldo, gs);
 }
 
 // K (input width) -> compile-time k-step count for the widths on the path
@@ -290,6 +306,7 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
   // each wave: at most ceil(16/NW) k-steps for K <= 256; issue all loads first
   constexpr int MAXS = (16 + NW - 1) / NW;
   f32x4 b[MAXS], a[MAXS][RB];
+  const float bias_v = (bias && (tid & 15) < N) ? bias[tid & 15] : 0.f;   // column (e & 15) == (tid & 15) below
 #pragma unroll
   for (int q = 0; q < MAXS; ++q) {
     const int s = wave + NW * q;
@@ -329,7 +346,7 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[(w * RB + rb) * 256 + rr * 16 + col];
-    const float z = v + (bias ? bias[col < N ? col : 0] : 0.f);
+    const float z = v + bias_v;
     const float y = act_fn<ACT>(z);
     const int row = rb * 16 + rr;
     if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
@@ -337,6 +354,148 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
       if (gs.gy) gs.gy[(size_t)row * gs.ldg + col] = y;
       if (gs.gz) gs.gz[(size_t)row * gs.ldg + col] = z;
     }
+  }
+}
+
+
+// Two independent layers on the SAME input tile, fused into one k-loop (e.g. the
+// dynamics model's diff and log-var heads, src/dynamics.py:84-91): column blocks
+// [0, NCB1) come from mirror P1 (N1 outputs -> out1), [NCB1, NCB1+NCB2) from P2
+// (N2 -> out2). One pass instead of two halves the layer's serial latency and
+// gives each wave more independent accumulators.
+template <int NW, int RB, int MAXC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K, const float* __restrict__ P1,
+                                                const float* __restrict__ b1, int N1, float* out1,
+                                                const float* __restrict__ P2, const float* __restrict__ b2, int N2,
+                                                float* out2, int ldo) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NCB1 = (N1 + 15) >> 4, NCB2 = (N2 + 15) >> 4;
+  const float* Pc[MAXC];
+  int cbs[MAXC];
+  float bvs[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int cb = min(wave + NW * c, NCB1 + NCB2 - 1);
+    const bool second = cb >= NCB1;
+    Pc[c] = second ? P2 : P1;
+    cbs[c] = second ? cb - NCB1 : cb;
+    const int col = cbs[c] * 16 + l15;
+    const float* bb = second ? b2 : b1;
+    const int nn = second ? N2 : N1;
+    bvs[c] = (bb && col < nn) ? bb[col] : 0.f;
+  }
+  f32x4 acc[RB][MAXC];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bq[PF_D][MAXC];
+#pragma unroll
+  for (int u = 0; u < PF_D - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(Pc[c], cbs[c], min(u, NK - 1), NK);
+  f32x4 an[RB], ac[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    if (s + PF_D - 1 < NK) {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) bq[(s + PF_D - 1) % PF_D][c] = load_pk(Pc[c], cbs[c], s + PF_D - 1, NK);
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
+    if (s + 1 < NK) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 16 * (s + 1) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF_D][c][m], acc[rb][c], 0, 0, 0);
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int cb = wave + NW * c;
+    if (cb >= NCB1 + NCB2) continue;
+    const bool second = cb >= NCB1;
+    float* out = second ? out2 : out1;
+    const int nn = second ? N2 : N1;
+    const int col = cbs[c] * 16 + l15;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * 16 + 4 * g + r;
+        out[row * ldo + col] = (col < nn) ? act_fn<ACT>(acc[rb][c][r] + bvs[c]) : 0.f;
+      }
+  }
+}
+
+// Two narrow layers (N1, N2 <= 16) on two input tiles at once: waves [0, NW/2) split
+// layer 1's K, waves [NW/2, NW) layer 2's; partials summed through `red`.
+template <int NW, int RB, int ACT>
+__device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const float* in2, int ldi, int K,
+                                                       const float* __restrict__ P1, const float* __restrict__ b1,
+                                                       int N1, float* out1, const float* __restrict__ P2,
+                                                       const float* __restrict__ b2, int N2, float* out2, int ldo,
+                                                       float* red) {
+  constexpr int HW = NW / 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NKS = (K + 15) >> 4;
+  const bool second = wave >= HW;
+  const int wl = second ? wave - HW : wave;
+  const float* P = second ? P2 : P1;
+  const float* in = second ? in2 : in1;
+  f32x4 acc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float bias1 = (b1 && (tid & 15) < N1) ? b1[tid & 15] : 0.f;
+  const float bias2 = (b2 && (tid & 15) < N2) ? b2[tid & 15] : 0.f;
+  constexpr int MAXS = (16 + HW - 1) / HW;      // K <= 256
+  f32x4 b[MAXS], a[MAXS][RB];
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    const int s = wl + HW * q;
+    const int sc = s < NKS ? s : 0;
+    b[q] = load_pk(P, 0, sc, NKS);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + sc * 16 + 4 * g);
+  }
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    if (wl + HW * q < NKS) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][rb][m], b[q][m], acc[rb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+  __syncthreads();
+  for (int e = tid; e < 2 * RB * 256; e += NW * 64) {
+    const int which = e / (RB * 256), e2 = e - which * RB * 256;
+    const int rb = e2 >> 8, rr = (e2 >> 4) & 15, col = e2 & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < HW; ++w) v += red[((which * HW + w) * RB + rb) * 256 + rr * 16 + col];
+    const int nn = which ? N2 : N1;
+    const float z = v + (which ? bias2 : bias1);
+    float* out = which ? out2 : out1;
+    out[(rb * 16 + rr) * ldo + col] = (col < nn) ? act_fn<ACT>(z) : 0.f;
   }
 }
 

@@ -91,6 +91,26 @@ __device__ inline int64_t prp_index(uint64_t i, uint64_t N, int hb, const uint32
   return (int64_t)(x % N);   // unreachable in practice (expected walk < 4)
 }
 
+#ifdef DRPO_STAMPS
+// profiling builds only (profiles/stamps.py): per-workgroup s_memtime stamps
+__device__ unsigned long long g_stamps_roll[1 << 14][16];
+#define RSTAMP(i)                                                                                 \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long _t;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) g_stamps_roll[blockIdx.x][(i)] = _t;         \
+  } while (0)
+DRPO_API int drpo_debug_stamps_rollout(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_roll), sizeof(unsigned long long) * 16 * (size_t)n);
+}
+#else
+#define RSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 template <int RB, int NW>
 __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p) {
   constexpr int ROWS = RB * 16;
@@ -103,7 +123,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   float* xin = smem;                       // ROWS x ldx  actor in / model in / next states
   float* h1 = xin + ROWS * p.ldx;          // ROWS x ldh
   float* h2 = h1 + ROWS * p.ldh;           // ROWS x ldh
-  float* sraw = h2 + ROWS * p.ldh;         // ROWS x lds  raw states
+  float* h3 = h2 + ROWS * p.ldh;           // ROWS x ldh  (log-var head hidden)
+  float* sraw = h3 + ROWS * p.ldh;         // ROWS x lds  raw states
   float* ao = sraw + ROWS * p.lds;         // ROWS x 20   actor head
   float* dout = ao + ROWS * 20;            // ROWS x ldm  diff head
   float* lout = dout + ROWS * p.ldm;       // ROWS x ldm  log-var head
@@ -115,7 +136,21 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   float* red = reinterpret_cast<float*>(srcrow + ROWS);    // NW*RB*256 narrow-layer partials
   int* s_part = reinterpret_cast<int*>(red + NW * RB * 256);   // NT scan partials
   int* scan = s_part + NT;                                 // prev tiles + 1 (exclusive prefix)
+  float* vecs = reinterpret_cast<float*>(scan + ((p.Bmax + ROWS - 1) / ROWS) + 1);   // 4 x 64: small vectors
+  float* v_nm = vecs;            // normalizer mean
+  float* v_ns = vecs + 64;       // normalizer std + 1e-6
+  float* v_lo = vecs + 128;      // min_log_var
+  float* v_hi = vecs + 192;      // max_log_var
+  // issue these tiny loads first: their latency hides behind the scan / gather
+  if (tid < 256) {
+    const int j = tid & 63, w = tid >> 6;
+    if (w == 0 && j < S) v_nm[j] = p.norm_mean[j];
+    if (w == 1 && j < S) v_ns[j] = p.norm_std[j] + 1e-6f;
+    if (w == 2 && j < S1) v_lo[j] = p.min_lv[j];
+    if (w == 3 && j < S1) v_hi[j] = p.max_lv[j];
+  }
 
+  RSTAMP(0);
   // ---- 0. row count / buffer offset of this step + compaction map ----------
   int n;
   int64_t off;
@@ -199,13 +234,17 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   }
   __syncthreads();
 
+  RSTAMP(1);
   // ---- 2. actor MLP (src/policy.py:61-100; mlp() ReLU hidden) ---------------
   tile_dense<NW, RB, MAXC, ACT_RELU>(xin, p.ldx, S, p.aW1, p.ab1, p.Ha, h1, p.ldh);
   __syncthreads();
+  RSTAMP(2);
   tile_dense<NW, RB, MAXC, ACT_RELU>(h1, p.ldh, p.Ha, p.aW2, p.ab2, p.Ha, h2, p.ldh);
   __syncthreads();
+  RSTAMP(3);
   tile_dense_narrow<NW, RB, ACT_NONE>(h2, p.ldh, p.Ha, p.aW3, p.ab3, 2 * A, ao, 20, red);
   __syncthreads();
+  RSTAMP(4);
 
   // ---- 3. squashed Gaussian sample + model input [normalize(s), a] ----------
   for (int e = tid; e < ROWS * A; e += NT) {
@@ -227,33 +266,55 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   }
   for (int e = tid; e < ROWS * S; e += NT) {
     const int r = e / S, k = e - r * S;
-    xin[r * p.ldx + k] = (sraw[r * p.lds + k] - p.norm_mean[k]) / (p.norm_std[k] + 1e-6f);
+    xin[r * p.ldx + k] = (sraw[r * p.lds + k] - v_nm[k]) / v_ns[k];
   }
   __syncthreads();
 
+  RSTAMP(5);
   // ---- 4. elite member forward (src/dynamics.py:112-122, swish) -------------
   tile_dense<NW, RB, MAXC, ACT_SILU>(xin, p.ldx, S + A, p.mW1, p.mb1, p.Hm, h1, p.ldh);
   __syncthreads();
+  RSTAMP(6);
   tile_dense<NW, RB, MAXC, ACT_SILU>(h1, p.ldh, p.Hm, p.mW2, p.mb2, p.Hm, h2, p.ldh);
   __syncthreads();
-  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.db1, p.Hm, h1, p.ldh);
-  __syncthreads();
-  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.ldm, red);
-  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.ldm);
-  __syncthreads();
-  tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.lb1, p.Hm, h1, p.ldh);
-  __syncthreads();
-  if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.lb2, S1, lout, p.ldm, red);
-  else tile_dense<NW, RB, 1, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.lb2, S1, lout, p.ldm);
-  __syncthreads();
+  RSTAMP(7);
+  if (S1 <= 16 && p.Hm == 200) {
+    // diff and log-var heads side by side: one fused hidden layer (2 x 13 column
+    // blocks, 4 per wave) and one fused split-K output layer
+    tile_dense_pair<NW, RB, (26 + NW - 1) / NW, ACT_SILU, 13>(h2, p.ldh, p.Hm, p.dW1, p.db1, p.Hm, h1, p.lW1,
+                                                               p.lb1, p.Hm, h3, p.ldh);
+    __syncthreads();
+    RSTAMP(8);
+    RSTAMP(9);
+    tile_dense_narrow_pair<NW, RB, ACT_NONE>(h1, h3, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.lW2, p.lb2, S1, lout,
+                                             p.ldm, red);
+    __syncthreads();
+    RSTAMP(10);
+    RSTAMP(11);
+  } else {
+    tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.dW1, p.db1, p.Hm, h1, p.ldh);
+    __syncthreads();
+    RSTAMP(8);
+    if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.ldm, red);
+    else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, p.ldh, p.Hm, p.dW2, p.db2, S1, dout, p.ldm);
+    __syncthreads();
+    RSTAMP(9);
+    tile_dense<NW, RB, MAXC, ACT_SILU>(h2, p.ldh, p.Hm, p.lW1, p.lb1, p.Hm, h1, p.ldh);
+    __syncthreads();
+    RSTAMP(10);
+    if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.lb2, S1, lout, p.ldm, red);
+    else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, p.ldh, p.Hm, p.lW2, p.lb2, S1, lout, p.ldm);
+    __syncthreads();
+    RSTAMP(11);
+  }
 
   // ---- 5. residual mean, log-var soft clamp, Gaussian sample ---------------
   for (int e = tid; e < ROWS * S1; e += NT) {
     const int r = e / S1, j = e - r * S1;
     const float mean = dout[r * p.ldm + j] + (j < S ? sraw[r * p.lds + j] : 0.f);
     float lv = lout[r * p.ldm + j];
-    lv = p.max_lv[j] - softplusf(p.max_lv[j] - lv);
-    lv = p.min_lv[j] + softplusf(lv - p.min_lv[j]);
+    lv = v_hi[j] - softplusf(v_hi[j] - lv);
+    lv = v_lo[j] + softplusf(lv - v_lo[j]);
     const float sd = sqrtf(expf(lv));
     float eps;
     if (p.eps_m) {
@@ -269,6 +330,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   }
   __syncthreads();
 
+  RSTAMP(12);
   // ---- 6. constraints + in-tile compaction ranks ---------------------------
   if (tid < 64) {
     bool alive_r = false;
@@ -286,10 +348,14 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   }
   __syncthreads();
 
+  RSTAMP(13);
   // ---- 7. row writes into the circular virtual buffer + next-state scratch --
+  int64_t* qrow = reinterpret_cast<int64_t*>(red);           // ROWS physical buffer rows (red is free now)
+  if (tid < rows) qrow[tid] = (vbase + tid) % p.vcap;
+  __syncthreads();
   for (int e = tid; e < rows * S; e += NT) {
     const int r = e / S, k = e - r * S;
-    const int64_t q = (vbase + r) % p.vcap;
+    const int64_t q = qrow[r];
     p.vs[q * S + k] = sraw[r * p.lds + k];
     const float x = xin[r * p.ldx + k];
     p.vs2[q * S + k] = x;
@@ -297,18 +363,19 @@ __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p
   }
   for (int e = tid; e < rows * A; e += NT) {
     const int r = e / A, d = e - r * A;
-    p.va[((vbase + r) % p.vcap) * A + d] = act[r * 8 + d];
+    p.va[qrow[r] * A + d] = act[r * 8 + d];
   }
   for (int e = tid; e < rows * C; e += NT) {
     const int r = e / C, c = e - r * C;
-    p.vh[((vbase + r) % p.vcap) * C + c] = hval[r * 8 + c];
+    p.vh[qrow[r] * C + c] = hval[r * 8 + c];
   }
   if (tid < rows) {
-    const int64_t q = (vbase + tid) % p.vcap;
+    const int64_t q = qrow[tid];
     p.vr[q] = rew[tid];
     p.vd[q] = flags[tid] & 1;
     p.vv[q] = (flags[tid] >> 1) & 1;
   }
+  RSTAMP(14);
 }
 
 // total rows written = off[H-1] + n[H-1]; advance the buffer pointer
@@ -424,8 +491,8 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
 
   const int tiles = (d->B + rpt - 1) / rpt;
   constexpr int NW = 8;
-  const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 2 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 2) +
-                                            (size_t)NW * (rpt / 16) * 256 + NW * 64 + (size_t)tiles + 1);
+  const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 3 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 2) +
+                                            (size_t)NW * (rpt / 16) * 256 + NW * 64 + (size_t)tiles + 1 + 256);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
 
   const int E_out_in[6][2] = {{d->Hm, S + A}, {d->Hm, d->Hm}, {d->Hm, d->Hm}, {S1, d->Hm}, {d->Hm, d->Hm}, {S1, d->Hm}};

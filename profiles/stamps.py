@@ -53,5 +53,39 @@ def main():
         buf[:] = 0
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and not os.environ.get('DRPO_STAMPS_ROLLOUT'):
     main()
+
+
+def rollout_stamps():
+    """Phase timing of rollout_step_kernel (step 1 of a steady-mode bench rollout)."""
+    import bench
+    from drpo_amd import _lib
+    L = _lib.lib()
+    L.drpo_debug_stamps_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device('cuda')
+    alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON)
+    rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
+    alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
+    alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
+    bench.steady_mode(alg)
+    alg.horizon = 1
+    for _ in range(3):
+        alg.rollout(alg.actor)
+    torch.cuda.synchronize()
+    buf = np.zeros((1 << 14, 16), np.uint64)
+    L.drpo_debug_stamps_rollout(buf.ctypes.data, 256)
+    st = buf[:256].astype(np.int64)
+    names = ['scan', 'gather', 'actor L1', 'actor L2', 'actor L3', 'sample', 'member L1', 'member L2', 'diff L1',
+             'diff L2', 'lv L1', 'lv L2', 'gauss', 'constraints', 'writes']
+    print('== rollout_step_kernel (B=4096, quadrotor): cycles per phase, mean over 256 workgroups')
+    tot = 0
+    for c in range(1, 15):
+        d = st[:, c] - st[:, c - 1]
+        tot += d.mean()
+        print(f'   {names[c]:12s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f}')
+    print(f'   total {tot:.0f} cycles')
+
+
+if __name__ == '__main__' and os.environ.get('DRPO_STAMPS_ROLLOUT'):
+    rollout_stamps()
