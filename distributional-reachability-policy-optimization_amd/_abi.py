@@ -53,6 +53,7 @@ class OptimSeg(ctypes.Structure):
 PROTOTYPES = {
     'drpo_version': (c_int, []),
     'drpo_last_error': (c_char_p, []),
+    'drpo_abi_sizeof': (c_int64, [c_char_p]),
     'drpo_rollout_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'drpo_rollout_count_offset': (c_size_t, [c_int, c_int, c_int]),
     'drpo_rollout': (c_int, [POINTER(RolloutDesc), P]),
@@ -100,11 +101,17 @@ class MlpNet(ctypes.Structure):
     _fields_ = [('nl', c_int), ('L', MlpLayer * 3)]
 
 
+class PolicyHead(ctypes.Structure):
+    """drpo_policy_head_t"""
+    _fields_ = [('mode', c_int), ('A', c_int), ('eps', P), ('site', ctypes.c_uint32), ('a', P), ('logp', P), ('u', P),
+                ('e', P), ('amean', P)]
+
+
 class MlpFwd(ctypes.Structure):
     """drpo_mlp_fwd_t"""
     _fields_ = [('src', P * 3), ('cols', c_int * 3), ('ld', c_int * 3), ('sstride', c_int64 * 3),
                 ('nmean', P), ('nstd', P), ('save_x', P), ('net', MlpNet * 3), ('nnets', c_int), ('trunk', c_int),
-                ('rows', c_int64), ('nbatch', c_int)]
+                ('rows', c_int64), ('nbatch', c_int), ('head', PolicyHead)]
 
 
 class MlpBwdLayer(ctypes.Structure):
@@ -148,6 +155,8 @@ class CriticHead(ctypes.Structure):
 
 PROTOTYPES.update({
     'drpo_mlp_forward': (c_int, [POINTER(MlpFwd), P]),
+    'drpo_mlp_forward_multi': (c_int, [POINTER(MlpFwd), P, c_int, c_uint64, c_uint64, P]),
+    'drpo_mlp_backward_multi': (c_int, [POINTER(MlpBwd), P, c_int, P]),
     'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
     'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P]),
     'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
@@ -159,7 +168,7 @@ PROTOTYPES.update({
     'drpo_critic_head': (c_int, [POINTER(CriticHead), P]),
     'drpo_actor_upstream': (c_int, [c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P, P, P, P, P, P, P, P,
                                     P]),
-    'drpo_squash_backward': (c_int, [c_int64, c_int, P, P, P, P, P, c_float, P, c_float, P, P, P]),
+    'drpo_squash_backward': (c_int, [c_int64, c_int, P, P, P, P, P, P, c_float, P, c_float, P, P, P]),
     'drpo_alpha_grad': (c_int, [P, P, c_int64, P, P]),
     'drpo_multiplier_head': (c_int, [c_int64, P, P, P, c_float, c_float, c_float, c_float, c_float, P, P, P]),
     'drpo_multiplier_out': (c_int, [c_int64, P, c_float, P, P]),

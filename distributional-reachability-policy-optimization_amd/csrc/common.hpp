@@ -104,6 +104,40 @@ __device__ __forceinline__ void philox_normal4(uint64_t seed, uint32_t c0, uint3
   out[2] = m2 * __builtin_amdgcn_cosf(u4); out[3] = m2 * __builtin_amdgcn_sinf(u4);
 }
 
+// element idx of a recorded draw array, or the Philox normal of (seed, ctr, site)
+__device__ __forceinline__ float normal_at(const float* eps, int64_t idx, uint64_t seed, uint64_t ctr, uint32_t site) {
+  if (eps) return eps[idx];
+  float z[4];
+  philox_normal4(seed, (uint32_t)(idx >> 2), (uint32_t)(idx >> 34), site, (uint32_t)ctr, z);
+  return z[idx & 3];
+}
+
+// squashed-Gaussian head of one row (src/policy.py:88-97; Independent(Tanh(Normal))
+// log_prob at the cached pre-tanh u). mode 0 sample, 1 rsample, 2 mean only.
+// raw = [mu | log-std pre-activation] (2A values, any stride source).
+template <typename RawAt>
+__device__ __forceinline__ void squashed_gaussian_row(RawAt raw_at, int64_t i, int A, int mode, const float* eps,
+                                                      uint64_t seed, uint64_t ctr, uint32_t site, float* a_out,
+                                                      float* logp, float* u_out, float* e_out, float* amean) {
+  float lp = 0.f;
+  for (int d = 0; d < A; ++d) {
+    const float mu = raw_at(d);
+    const float ls = -6.f + 10.f * sigmoidf(raw_at(A + d));
+    const float sd = expf(ls) * 1.0f;
+    if (amean) amean[i * A + d] = tanhf(mu);
+    if (mode == 2) continue;
+    const float e = normal_at(eps, i * A + d, seed, ctr, site);
+    const float u = (mode == 0) ? e * sd + mu : mu + e * sd;
+    if (a_out) a_out[i * A + d] = tanhf(u);
+    if (u_out) u_out[i * A + d] = u;
+    if (e_out) e_out[i * A + d] = e;
+    const float ladj = 2.f * (0.69314718055994531f - u - softplusf(-2.f * u));
+    const float base = -((u - mu) * (u - mu)) / (2.f * (sd * sd)) - logf(sd) - 0.91893853320467274f;
+    lp += (0.f - ladj) + base;
+  }
+  if (logp && mode != 2) logp[i] = lp;
+}
+
 // ---------------------------------------------------------------------------
 // tile_dense: out[r][c] = act(sum_k in[r][k] * W[c][k] + b[c]) for a tile of RB*16
 // rows. `in` / `out` are LDS tiles with row strides ldi / ldo; columns

@@ -1,6 +1,7 @@
 // Library-wide C ABI: version, error reporting.
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "common.hpp"
 
@@ -44,4 +45,22 @@ DRPO_API int drpo_event_elapsed_ms(float* ms, void* start, void* stop) {
     return DRPO_EHIP;
   }
   return DRPO_OK;
+}
+
+// sizeof of every ABI struct by name (binding self-check: tests/test_abi.py compares
+// these with the ctypes mirrors); -1 for an unknown name
+DRPO_API int64_t drpo_abi_sizeof(const char* name) {
+  struct E { const char* n; size_t s; };
+  static const E table[] = {
+      {"drpo_rollout_desc_t", sizeof(drpo_rollout_desc_t)}, {"drpo_mlp_layer_t", sizeof(drpo_mlp_layer_t)},
+      {"drpo_mlp_net_t", sizeof(drpo_mlp_net_t)},           {"drpo_policy_head_t", sizeof(drpo_policy_head_t)},
+      {"drpo_mlp_fwd_t", sizeof(drpo_mlp_fwd_t)},           {"drpo_mlp_bwd_layer_t", sizeof(drpo_mlp_bwd_layer_t)},
+      {"drpo_mlp_bwd_net_t", sizeof(drpo_mlp_bwd_net_t)},   {"drpo_mlp_bwd_t", sizeof(drpo_mlp_bwd_t)},
+      {"drpo_wgrad_item_t", sizeof(drpo_wgrad_item_t)},     {"drpo_buffer_view_t", sizeof(drpo_buffer_view_t)},
+      {"drpo_critic_head_t", sizeof(drpo_critic_head_t)},   {"drpo_pack_item_t", sizeof(drpo_pack_item_t)},
+      {"drpo_pack_map_t", sizeof(drpo_pack_map_t)},         {"drpo_optim_seg_t", sizeof(drpo_optim_seg_t)},
+  };
+  for (const E& e : table)
+    if (strcmp(e.n, name) == 0) return (int64_t)e.s;
+  return -1;
 }

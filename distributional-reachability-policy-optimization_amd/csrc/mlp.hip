@@ -167,6 +167,137 @@ static int check_net(const drpo_mlp_net_t& n, int din) {
   return 1;
 }
 
+// ---------------------------------------------------------------------------
+// multi-job forward: several independent forwards in one launch
+// ---------------------------------------------------------------------------
+// Job descriptors live in device memory (built once per workspace layout and read
+// with scalar loads), grid.y enumerates (job, net) slots, grid.x row tiles. The
+// latency chain of one 16-row tile (stage -> layer -> layer -> ...) is serial, so
+// running e.g. the actor, safe actor, twin critics and constraint critic of one
+// SAC loss in one launch puts 4 such chains on every CU at once.
+namespace {
+constexpr int MJ_MAXSLOT = 16;
+}
+struct MultiArgs {
+  const drpo_mlp_fwd_t* jobs;
+  unsigned char slot_job[MJ_MAXSLOT], slot_net[MJ_MAXSLOT];
+  uint64_t seed, ctr;
+};
+
+__device__ __forceinline__ float* run_net_g(const drpo_mlp_fwd_t* __restrict__ a, int ni, float* in, float* bufA,
+                                            float* bufB, int z, int row0, int nrows, float* red) {
+  float* cur = in;
+  const int nl = a->net[ni].nl;
+  for (int l = 0; l < nl; ++l) {
+    float* out = (cur == bufA) ? bufB : bufA;
+    run_layer(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
+    __syncthreads();
+    cur = out;
+  }
+  return cur;
+}
+
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_fwd_multi_kernel(MultiArgs m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* xin = smem;
+  float* bA = xin + FW_ROWS * LDH;
+  float* bB = bA + FW_ROWS * LDH;
+  float* T = bB + FW_ROWS * LDH;
+  float* red = T + FW_ROWS * LDH;
+  const drpo_mlp_fwd_t* __restrict__ a = m.jobs + m.slot_job[blockIdx.y];
+  const int net = m.slot_net[blockIdx.y];
+  const int tid = threadIdx.x;
+  const int z = blockIdx.z;
+  const int row0 = blockIdx.x * FW_ROWS;
+  if (row0 >= a->rows || z >= a->nbatch) return;
+  const int nrows = (int)min((int64_t)FW_ROWS, a->rows - row0);
+  const int c0 = a->cols[0], c1 = a->cols[1];
+  const int din0 = c0 + c1 + a->cols[2];
+  const int kpad = round_up(din0, 16);
+  for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
+    const int r = e / kpad, k = e - r * kpad;
+    float v = 0.f;
+    if (r < nrows && k < din0) {
+      const int64_t row = row0 + r;
+      const int q = k < c0 ? 0 : (k - c0 < c1 ? 1 : 2);
+      const int kk = q == 0 ? k : (q == 1 ? k - c0 : k - c0 - c1);
+      v = a->src[q][(size_t)z * a->sstride[q] + row * a->ld[q] + kk];
+      if (q == 0 && a->nmean) v = (v - a->nmean[kk]) / (a->nstd[kk] + 1e-6f);
+      if (a->save_x) a->save_x[((size_t)z * a->rows + row) * din0 + k] = v;
+    }
+    xin[r * LDH + k] = v;
+  }
+  __syncthreads();
+  float* outp;
+  if (!a->trunk) {
+    outp = run_net_g(a, net, xin, bA, bB, z, row0, nrows, red);
+  } else {
+    float* t = run_net_g(a, 0, xin, bA, bB, z, row0, nrows, red);
+    const int w = a->net[0].L[a->net[0].nl - 1].dout;
+    const int wpad = round_up(w, 16);
+    for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
+      const int r = e / wpad, k = e - r * wpad;
+      T[r * LDH + k] = t[r * LDH + k];
+    }
+    __syncthreads();
+    outp = nullptr;
+    for (int h = 1; h < a->nnets; ++h) run_net_g(a, h, T, bA, bB, z, row0, nrows, red);
+  }
+  // fused squashed-Gaussian head on net 0's output (non-trunk jobs)
+  const drpo_policy_head_t& hd = a->head;
+  if (hd.mode != 0 && outp && net == 0 && tid < nrows) {
+    const float* rrow = outp + tid * LDH;
+    squashed_gaussian_row([&](int c) { return rrow[c]; }, (int64_t)(row0 + tid), hd.A, hd.mode - 1, hd.eps, m.seed,
+                          m.ctr, hd.site, hd.a, hd.logp, hd.u, hd.e, hd.amean);
+  }
+}
+
+DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_mlp_fwd_t* jobs_dev, int njobs,
+                                    uint64_t seed, uint64_t ctr, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(jobs_host && jobs_dev && njobs >= 1 && njobs <= 8, "drpo_mlp_forward_multi: 1..8 jobs");
+  MultiArgs m{};
+  m.jobs = jobs_dev;
+  m.seed = seed;
+  m.ctr = ctr;
+  int slots = 0;
+  int64_t tiles = 0;
+  int nbatch = 1;
+  for (int j = 0; j < njobs; ++j) {
+    const drpo_mlp_fwd_t* a = jobs_host + j;
+    DRPO_REQUIRE(a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_forward_multi: bad job %d", j);
+    const int din0 = a->cols[0] + a->cols[1] + a->cols[2];
+    DRPO_REQUIRE(din0 >= 1 && din0 <= 256, "drpo_mlp_forward_multi: job %d input width %d", j, din0);
+    if (a->trunk) {
+      DRPO_REQUIRE(check_net(a->net[0], din0), "drpo_mlp_forward_multi: job %d bad trunk", j);
+      const int tw = a->net[0].L[a->net[0].nl - 1].dout;
+      for (int h = 1; h < a->nnets; ++h)
+        DRPO_REQUIRE(check_net(a->net[h], tw), "drpo_mlp_forward_multi: job %d bad head %d", j, h);
+      DRPO_REQUIRE(a->head.mode == 0, "drpo_mlp_forward_multi: policy head on a trunk job");
+    } else {
+      for (int h = 0; h < a->nnets; ++h)
+        DRPO_REQUIRE(check_net(a->net[h], din0), "drpo_mlp_forward_multi: job %d bad net %d", j, h);
+    }
+    if (a->head.mode != 0)
+      DRPO_REQUIRE(a->head.mode <= 3 && a->head.A >= 1 && 2 * a->head.A == a->net[0].L[a->net[0].nl - 1].dout,
+                   "drpo_mlp_forward_multi: job %d policy head shape", j);
+    const int ns = a->trunk ? 1 : a->nnets;
+    DRPO_REQUIRE(slots + ns <= MJ_MAXSLOT, "drpo_mlp_forward_multi: too many nets");
+    for (int h = 0; h < ns; ++h) {
+      m.slot_job[slots] = (unsigned char)j;
+      m.slot_net[slots] = (unsigned char)h;
+      ++slots;
+    }
+    tiles = max(tiles, (a->rows + FW_ROWS - 1) / FW_ROWS);
+    nbatch = max(nbatch, a->nbatch);
+  }
+  if (tiles == 0) return DRPO_OK;
+  mlp_fwd_multi_kernel<<<dim3((unsigned)tiles, slots, nbatch), FW_NT, fwd_lds(), stream>>>(m);
+  DRPO_LAUNCH_CHECK("mlp_forward_multi");
+  return DRPO_OK;
+}
+
+
 DRPO_API int drpo_mlp_forward(const drpo_mlp_fwd_t* a, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_forward: bad descriptor");
@@ -235,8 +366,9 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* 
   return cur;
 }
 
-__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+// one (job, net) slot of the fused backward-data pass; `a` may live in kernarg
+// (single launch) or global memory (multi-job launch)
+__device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& a, int sel, float* smem) {
   float* G = smem;
   float* bA = G + FW_ROWS * LDH;
   float* bB = bA + FW_ROWS * LDH;
@@ -267,7 +399,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   };
 
   if (!a.trunk) {
-    const drpo_mlp_bwd_net_t& n = a.net[blockIdx.y];
+    const drpo_mlp_bwd_net_t& n = a.net[sel];
     load_gout(n, G);
     const float* gx = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, n.dx != nullptr);
     if (gx) store_dx(n, gx);
@@ -290,6 +422,24 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   if (gx) store_dx(a.net[0], gx);
 }
 
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  bwd_body(a, blockIdx.y, smem);
+}
+
+struct BwdMultiArgs {
+  const drpo_mlp_bwd_t* jobs;
+  unsigned char slot_job[16], slot_net[16];
+};
+
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_multi_kernel(
+    BwdMultiArgs m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const drpo_mlp_bwd_t& a = m.jobs[m.slot_job[blockIdx.y]];
+  if (blockIdx.z >= (unsigned)a.nbatch) return;
+  bwd_body(a, m.slot_net[blockIdx.y], smem);
+}
+
 static size_t bwd_lds() { return sizeof(float) * (size_t)4 * FW_ROWS * LDH; }
 
 DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, drpo_stream_t stream_) {
@@ -308,6 +458,45 @@ DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, drpo_stream_t stream_) {
   dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS), a->trunk ? 1 : a->nnets, a->nbatch);
   mlp_bwd_kernel<<<grid, FW_NT, bwd_lds(), stream>>>(*a);
   DRPO_LAUNCH_CHECK("mlp_backward");
+  return DRPO_OK;
+}
+
+static int check_bwd(const drpo_mlp_bwd_t* a) {
+  if (!(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1)) return 0;
+  for (int h = 0; h < a->nnets; ++h) {
+    const drpo_mlp_bwd_net_t& n = a->net[h];
+    if (!(n.nl >= 1 && n.nl <= MAXL && (n.gout || (a->trunk && h == 0)))) return 0;
+    for (int l = 0; l < n.nl; ++l)
+      if (!(n.L[l].din >= 1 && n.L[l].din <= 256 && n.L[l].dout >= 1 && n.L[l].dout <= 256 && n.L[l].W)) return 0;
+    if (n.dx && !(n.dx_col0 >= 0 && n.dx_col0 + n.dx_cols <= n.L[0].din)) return 0;
+  }
+  return 1;
+}
+
+DRPO_API int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                                     drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(jobs_host && jobs_dev && njobs >= 1 && njobs <= 8, "drpo_mlp_backward_multi: 1..8 jobs");
+  BwdMultiArgs m{};
+  m.jobs = jobs_dev;
+  int slots = 0, nbatch = 1;
+  int64_t tiles = 0;
+  for (int j = 0; j < njobs; ++j) {
+    const drpo_mlp_bwd_t* a = jobs_host + j;
+    DRPO_REQUIRE(check_bwd(a), "drpo_mlp_backward_multi: bad job %d", j);
+    const int ns = a->trunk ? 1 : a->nnets;
+    DRPO_REQUIRE(slots + ns <= 16, "drpo_mlp_backward_multi: too many nets");
+    for (int h = 0; h < ns; ++h) {
+      m.slot_job[slots] = (unsigned char)j;
+      m.slot_net[slots] = (unsigned char)h;
+      ++slots;
+    }
+    tiles = max(tiles, (a->rows + FW_ROWS - 1) / FW_ROWS);
+    nbatch = max(nbatch, a->nbatch);
+  }
+  if (tiles == 0) return DRPO_OK;
+  mlp_bwd_multi_kernel<<<dim3((unsigned)tiles, slots, nbatch), FW_NT, bwd_lds(), stream>>>(m);
+  DRPO_LAUNCH_CHECK("mlp_backward_multi");
   return DRPO_OK;
 }
 

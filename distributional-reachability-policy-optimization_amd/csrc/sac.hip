@@ -38,12 +38,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;   // valid in thread 0
 }
 
-__device__ __forceinline__ float normal_at(const float* eps, int64_t idx, uint64_t seed, uint64_t ctr, uint32_t site) {
-  if (eps) return eps[idx];
-  float z[4];
-  philox_normal4(seed, (uint32_t)(idx >> 2), (uint32_t)(idx >> 34), site, (uint32_t)ctr, z);
-  return z[idx & 3];
-}
 
 __device__ __forceinline__ float cc_std(float l, float lmin, float lmax) {
   float ls = lmax - softplusf(lmax - l);
@@ -129,29 +123,19 @@ __global__ void policy_head_kernel(const float* raw, int64_t B, int A, int mode,
                                    float* amean) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  float lp = 0.f;
-  for (int d = 0; d < A; ++d) {
-    const float mu = raw[i * 2 * A + d];
-    const float ls = -6.f + 10.f * sigmoidf(raw[i * 2 * A + A + d]);
-    const float sd = expf(ls) * 1.0f;
-    if (amean) amean[i * A + d] = tanhf(mu);
-    if (mode == 3) {   // distribution parameters (loc, scale) for distr()
+  const float* r = raw + i * 2 * A;
+  if (mode == 3) {   // distribution parameters (loc, scale) for distr()
+    for (int d = 0; d < A; ++d) {
+      const float mu = r[d];
+      const float sd = expf(-6.f + 10.f * sigmoidf(r[A + d])) * 1.0f;
+      if (amean) amean[i * A + d] = tanhf(mu);
       if (u_out) u_out[i * A + d] = mu;
       if (e_out) e_out[i * A + d] = sd;
-      continue;
     }
-    if (mode == 2) continue;
-    const float e = normal_at(eps, i * A + d, seed, ctr, site);
-    const float u = (mode == 0) ? e * sd + mu : mu + e * sd;
-    if (a_out) a_out[i * A + d] = tanhf(u);
-    if (u_out) u_out[i * A + d] = u;
-    if (e_out) e_out[i * A + d] = e;
-    // Independent(TransformedDistribution(Normal, Tanh)).log_prob at the cached u
-    const float ladj = 2.f * (0.69314718055994531f - u - softplusf(-2.f * u));
-    const float base = -((u - mu) * (u - mu)) / (2.f * (sd * sd)) - logf(sd) - 0.91893853320467274f;
-    lp += (0.f - ladj) + base;
+    return;
   }
-  if (logp && mode < 2) logp[i] = lp;
+  squashed_gaussian_row([&](int c) { return r[c]; }, i, A, mode, eps, seed, ctr, site, a_out, logp, u_out, e_out,
+                        amean);
 }
 
 DRPO_API int drpo_policy_head(const float* raw, int64_t B, int A, int mode, const float* eps, uint64_t seed,
@@ -361,7 +345,7 @@ DRPO_API int drpo_actor_upstream(int64_t B, int C, int distributional, float std
 // Writes draw [B][2A] = dL/d(mu, raw log-std). Optionally accumulates
 // sum_i (logp_i + target_entropy) into *alpha_sum (alpha loss).
 __global__ __launch_bounds__(256) void squash_bwd_kernel(int64_t B, int A, const float* raw, const float* u,
-                                                         const float* e, const float* dA, const float* log_alpha,
+                                                         const float* e, const float* dA, const float* dA2, const float* log_alpha,
                                                          float lp_scale, const float* logp, float target_entropy,
                                                          float* alpha_sum, float* draw) {
   __shared__ float red[8];
@@ -377,7 +361,8 @@ __global__ __launch_bounds__(256) void squash_bwd_kernel(int64_t B, int A, const
       const float a = tanhf(uu);
       const float diff = uu - mu;
       const float var = sd * sd;
-      const float du = dA[i * A + d] * (1.f - a * a) + glp * (-diff / var + 2.f - 4.f * sp_grad(-2.f * uu));
+      const float dAv = dA2 ? dA[i * A + d] + dA2[i * A + d] : dA[i * A + d];
+      const float du = dAv * (1.f - a * a) + glp * (-diff / var + 2.f - 4.f * sp_grad(-2.f * uu));
       const float dmu = du + glp * diff / var;
       const float dsd = du * ee + glp * (diff * diff / (var * sd) - 1.f / sd);
       draw[i * 2 * A + d] = dmu;
@@ -391,12 +376,12 @@ __global__ __launch_bounds__(256) void squash_bwd_kernel(int64_t B, int A, const
   }
 }
 
-DRPO_API int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, const float* e, const float* dA,
+DRPO_API int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, const float* e, const float* dA, const float* dA2,
                                   const float* log_alpha, float lp_scale, const float* logp, float target_entropy,
                                   float* alpha_sum, float* draw, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
-  squash_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(B, A, raw, u, e, dA, log_alpha, lp_scale, logp,
+  squash_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(B, A, raw, u, e, dA, dA2, log_alpha, lp_scale, logp,
                                                                      target_entropy, alpha_sum, draw);
   DRPO_LAUNCH_CHECK("squash_backward");
   return DRPO_OK;

@@ -39,6 +39,7 @@ enum { DRPO_ENV_POINT_ROBOT = 0, DRPO_ENV_QUADROTOR = 1, DRPO_ENV_CARTPOLE = 2, 
 
 /* ---------------------------------------------------------------- library */
 int drpo_version(void);
+int64_t drpo_abi_sizeof(const char* struct_name);   /* binding self-check */
 const char* drpo_last_error(void);
 int drpo_event_create(void** ev);
 int drpo_event_destroy(void* ev);
@@ -110,6 +111,16 @@ typedef struct {
   drpo_mlp_layer_t L[3];
 } drpo_mlp_net_t;
 
+/* squashed-Gaussian policy head fused into a forward pass: applied to net[0]'s
+ * final output (2A columns = [mu | log-std pre-activation]), src/policy.py:88-97 */
+typedef struct {
+  int mode;            /* 0 none, 1 sample (Normal.sample), 2 rsample, 3 mean only (tanh(mu)) */
+  int A;
+  const float* eps;    /* [rows][A] recorded draws, or NULL: Philox (launch seed/ctr, this site) */
+  uint32_t site;
+  float *a, *logp, *u, *e, *amean;   /* optional outputs */
+} drpo_policy_head_t;
+
 typedef struct {
   const float* src[3]; /* column-concatenated input sources (e.g. torch.cat([s, a], -1)) */
   int cols[3];
@@ -123,6 +134,7 @@ typedef struct {
   int trunk;           /* 1: net[0] trunk, net[1..] heads on its output */
   int64_t rows;
   int nbatch;
+  drpo_policy_head_t head;   /* multi-job launches only (mode 0 elsewhere) */
 } drpo_mlp_fwd_t;
 
 typedef struct {
@@ -162,7 +174,16 @@ typedef struct {
 } drpo_wgrad_item_t;
 
 int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);
+/* Up to 8 independent forward jobs (different inputs / nets, e.g. every forward of
+ * one SAC loss that does not depend on another) in ONE launch, each with an
+ * optional fused policy head. jobs_dev: the same descriptors in device memory
+ * (read by the kernel; static across calls), jobs_host: for the grid. */
+int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_mlp_fwd_t* jobs_dev, int njobs, uint64_t seed,
+                           uint64_t ctr, drpo_stream_t stream);
 int drpo_mlp_backward(const drpo_mlp_bwd_t* desc /* host */, drpo_stream_t stream);
+/* independent backward-data jobs in one launch (descriptors in device memory) */
+int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                            drpo_stream_t stream);
 int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- packed weight mirrors
@@ -242,7 +263,7 @@ int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, f
 
 /* chain rule through rsample/tanh/log_prob to the actor head; alpha-loss sum */
 int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, const float* e, const float* dA,
-                         const float* log_alpha, float lp_scale, const float* logp, float target_entropy,
+                         const float* dA2 /* optional second dL/da term, summed: dA + dA2 */, const float* log_alpha, float lp_scale, const float* logp, float target_entropy,
                          float* alpha_sum, float* draw, drpo_stream_t stream);
 
 /* d alpha_loss / d log_alpha (src/ssac.py:498-501) */

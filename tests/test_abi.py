@@ -69,3 +69,16 @@ def test_device_entry_points_refuse_without_gpu():
         pytest.skip('GPU present')
     with pytest.raises(_lib.DrpoError):
         _lib.require_device(torch.zeros(1))
+
+
+def test_struct_layouts_match(built):
+    """Every ctypes mirror has the C struct's size (catches field drift in either)."""
+    from drpo_amd import _abi as A
+    pairs = {'drpo_rollout_desc_t': A.RolloutDesc, 'drpo_mlp_layer_t': A.MlpLayer, 'drpo_mlp_net_t': A.MlpNet,
+             'drpo_policy_head_t': A.PolicyHead, 'drpo_mlp_fwd_t': A.MlpFwd, 'drpo_mlp_bwd_layer_t': A.MlpBwdLayer,
+             'drpo_mlp_bwd_net_t': A.MlpBwdNet, 'drpo_mlp_bwd_t': A.MlpBwd, 'drpo_wgrad_item_t': A.WgradItem,
+             'drpo_buffer_view_t': A.BufferView, 'drpo_critic_head_t': A.CriticHead,
+             'drpo_pack_item_t': A.PackItem, 'drpo_pack_map_t': A.PackMap, 'drpo_optim_seg_t': A.OptimSeg}
+    for name, cls in pairs.items():
+        assert built.drpo_abi_sizeof(name.encode()) == ctypes.sizeof(cls), name
+    assert built.drpo_abi_sizeof(b'nope') == -1
