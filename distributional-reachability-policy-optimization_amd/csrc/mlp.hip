@@ -62,7 +62,7 @@ __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const dr
     tile_dense<FW_NW, 1, FW_MAXC, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, gs);
 }
 
-__device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& L, int z, int64_t rows,
+__device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& __restrict__ L, int z, int64_t rows,
                                           int row0, int nrows, float* out, float* red) {
   const float* W = L.W + (size_t)z * L.wstride;
   const float* b = L.b + (size_t)z * L.bstride;
@@ -333,33 +333,39 @@ __device__ __forceinline__ float act_grad(int act, float y, float z) {
 }
 
 // G (LDS, width of the net output) -> gradient w.r.t. the net input (returned LDS buffer)
-__device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* G, float* bA, float* bB, int z, int64_t rows,
+__device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__ net, float* G, float* bA, float* bB, int z, int64_t rows,
                           int row0, int nrows, bool need_dx0) {
   const int tid = threadIdx.x;
   float* cur = G;
   for (int l = net.nl - 1; l >= 0; --l) {
     const drpo_mlp_bwd_layer_t& L = net.L[l];
-    const size_t so = ((size_t)z * rows + row0) * L.dout;
-    const int wpad = round_up(L.dout, 16);
+    // descriptor fields into registers once per layer (no reloads inside the loops)
+    const int dout = L.dout, din = L.din, act = L.act;
+    const float* __restrict__ sy = L.sy;
+    const float* __restrict__ sz = L.sz;
+    float* __restrict__ dzp = L.dz;
+    const float* W = L.W + (size_t)z * L.wstride;
+    const size_t so = ((size_t)z * rows + row0) * dout;
+    const int wpad = round_up(dout, 16);
+#pragma unroll 8
     for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
       const int r = e / wpad, k = e - r * wpad;
       float g = 0.f;
-      if (r < nrows && k < L.dout) {
+      if (r < nrows && k < dout) {
         g = cur[r * LDH + k];
-        if (L.act != ACT_NONE) {
-          const size_t idx = so + (size_t)r * L.dout + k;
-          g *= act_grad(L.act, L.sy ? L.sy[idx] : 0.f, L.sz ? L.sz[idx] : 0.f);
+        if (act != ACT_NONE) {
+          const size_t idx = so + (size_t)r * dout + k;
+          g *= act_grad(act, sy ? sy[idx] : 0.f, sz ? sz[idx] : 0.f);
         }
-        if (L.dz) L.dz[so + (size_t)r * L.dout + k] = g;
+        if (dzp) dzp[so + (size_t)r * dout + k] = g;
       }
       cur[r * LDH + k] = g;
     }
     __syncthreads();
     if (l == 0 && !need_dx0) return nullptr;   // input gradient not wanted: dZ_0 (saved) is all wgrad needs
     float* out = (cur == bA) ? bB : bA;
-    const float* W = L.W + (size_t)z * L.wstride;
     // dY_prev = dZ W: transposed mirror, N = din, K = dout
-    tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, L.dout, W, nullptr, L.din, out, LDH);
+    tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, dout, W, nullptr, din, out, LDH);
     __syncthreads();
     cur = out;
   }
@@ -368,7 +374,7 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& net, float* 
 
 // one (job, net) slot of the fused backward-data pass; `a` may live in kernarg
 // (single launch) or global memory (multi-job launch)
-__device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& a, int sel, float* smem) {
+__device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, int sel, float* smem) {
   float* G = smem;
   float* bA = G + FW_ROWS * LDH;
   float* bB = bA + FW_ROWS * LDH;
@@ -435,7 +441,8 @@ struct BwdMultiArgs {
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_multi_kernel(
     BwdMultiArgs m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const drpo_mlp_bwd_t& a = m.jobs[m.slot_job[blockIdx.y]];
+  const drpo_mlp_bwd_t* __restrict__ ap = m.jobs + m.slot_job[blockIdx.y];
+  const drpo_mlp_bwd_t& a = *ap;
   if (blockIdx.z >= (unsigned)a.nbatch) return;
   bwd_body(a, m.slot_net[blockIdx.y], smem);
 }

@@ -66,6 +66,11 @@ def _p(t):
     return 0 if t is None else t.data_ptr()
 
 
+def noise_tag(eps):
+    """descriptor-cache suffix: recorded draws (parity) vs Philox (production)"""
+    return '.p' if eps is not None else '.d'
+
+
 def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, wstride=None, sstride=None):
     d = MlpFwd()
     for k, (t, cols) in enumerate(srcs):
@@ -102,6 +107,17 @@ def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None):
             t, c0, nc, accum = dx[j]
             d.net[j].dx, d.net[j].dx_col0, d.net[j].dx_cols, d.net[j].dx_accumulate = t.data_ptr(), c0, nc, int(accum)
     d.nnets, d.trunk, d.rows, d.nbatch = len(nets), int(trunk), rows, nbatch
+    return d
+
+
+HEAD_SAMPLE, HEAD_RSAMPLE, HEAD_MEAN = 1, 2, 3
+
+
+def with_head(d, mode, A, eps, site, a=None, logp=None, u=None, e=None, amean=None):
+    """Attach a fused squashed-Gaussian head (drpo_policy_head_t) to a forward descriptor."""
+    h = d.head
+    h.mode, h.A, h.eps, h.site = mode, A, _p(eps), site
+    h.a, h.logp, h.u, h.e, h.amean = _p(a), _p(logp), _p(u), _p(e), _p(amean)
     return d
 
 
@@ -291,6 +307,36 @@ class SACEngine:
         if ev:
             self.profiler.end(ev)
 
+    def _upload(self, structs):
+        raw = bytes(structs)
+        return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.dev)
+
+    def _run_multi(self, key, builder, ctr):
+        """Independent forwards (+ fused policy heads) in one launch; descriptors are
+        built once and kept in device memory."""
+        d = self.desc.get(key)
+        if d is None:
+            jobs = builder()
+            arr = (MlpFwd * len(jobs))(*jobs)
+            d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(fwd_flops(j) for j in jobs))
+        arr, dev, nj, fl = d
+        ev = self.profiler.begin('mlp_fwd', key, fl) if self.profiler else None
+        _lib.check(_lib.lib().drpo_mlp_forward_multi(arr, dev.data_ptr(), nj, self.noise.seed, ctr, _lib.stream()), key)
+        if ev:
+            self.profiler.end(ev)
+
+    def _run_bwd_multi(self, key, builder):
+        d = self.desc.get(key)
+        if d is None:
+            jobs = builder()
+            arr = (MlpBwd * len(jobs))(*jobs)
+            d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(bwd_flops(j) for j in jobs))
+        arr, dev, nj, fl = d
+        ev = self.profiler.begin('mlp_bwd', key, fl) if self.profiler else None
+        _lib.check(_lib.lib().drpo_mlp_backward_multi(arr, dev.data_ptr(), nj, _lib.stream()), key)
+        if ev:
+            self.profiler.end(ev)
+
     def _run_bwd(self, key, builder):
         d = self.desc.get(key)
         if d is None:
@@ -372,12 +418,6 @@ class SACEngine:
         noise.randn_like(qshape, used=False)       # loss forward's unused draw (src/ssac.py:80)
         ctr = noise.next()
         ws = self.ws
-        # target policy sample a' ~ pi(s'), log pi
-        self._run_fwd('c.actor', lambda: fill_fwd([self._out_net(n['actor'], 'c.raw_a', B)],
-                                                  [(self.bs2, S), (None, 0), (None, 0)], B))
-        self._policy_head(ws['c.raw_a'], 0, e1, SITE_PI_NEXT, ctr, a=self.buf('c.a2', B, A), logp=self.buf('c.lp2', B))
-        self._run_fwd('c.qt', lambda: fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (ws['c.a2'], A), (None, 0)], B))
-        # safe policy sample on s' (robust: on the model's s')
         s2c, rk = self.bs2, ''
         if robust:
             s2c, rk = self.buf('c.s2m', B, S), '.r'
@@ -389,17 +429,21 @@ class SACEngine:
                                               ep['quad_x_threshold'], ep['quad_z_threshold'], s2c.data_ptr(), B, S,
                                               dm.data_ptr(), self.buf('c.vm', B, dtype=torch.uint8).data_ptr(),
                                               self.buf('c.hm', B, C).data_ptr(), _lib.stream()), 'env_constraints')
-        self._run_fwd('c.safe' + rk, lambda: fill_fwd([self._out_net(n['safe'], 'c.raw_s', B)],
-                                                      [(s2c, S), (None, 0), (None, 0)], B))
-        self._policy_head(ws['c.raw_s'], 0, e2, SITE_SAFE_NEXT, ctr, a=self.buf('c.a2s', B, A))
-        self._run_fwd('c.cct' + rk, lambda: fill_fwd(self._cc_nets('t'), [(s2c, S), (ws['c.a2s'], A), (None, 0)], B,
-                                                     trunk=True))
-        # critics and constraint critic at (s, a) with saves
         xs = self.buf('c.x', B, S + A)
-        self._run_fwd('c.q', lambda: fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B,
-                                              save_x=xs))
-        self._run_fwd('c.cc', lambda: fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B,
-                                               trunk=True))
+        a2, lp2, a2s = self.buf('c.a2', B, A), self.buf('c.lp2', B), self.buf('c.a2s', B, A)
+        # launch 1: a' ~ pi(s') with log pi, a'_safe ~ pi_safe(s') (robust: model s'), and
+        # the twin critics + constraint critic at (s, a) with their backward saves
+        self._run_multi('c.f1' + rk + noise_tag(e1), lambda: [
+            with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs2, S), (None, 0), (None, 0)], B), HEAD_SAMPLE, A,
+                      e1, SITE_PI_NEXT, a=a2, logp=lp2),
+            with_head(fill_fwd([Net(n['safe'].layers)], [(s2c, S), (None, 0), (None, 0)], B), HEAD_SAMPLE, A, e2,
+                      SITE_SAFE_NEXT, a=a2s),
+            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs),
+            fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True)], ctr)
+        # launch 2: target critics at (s', a') and target constraint critic at (s', a'_safe)
+        self._run_multi('c.f2' + rk, lambda: [
+            fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (a2, A), (None, 0)], B),
+            fill_fwd(self._cc_nets('t'), [(s2c, S), (a2s, A), (None, 0)], B, trunk=True)], ctr)
         loss = self._loss_slots(2)
         self._clean_grads(sol.critic_group)
         ch = self.desc.get('c.head')
@@ -424,10 +468,10 @@ class SACEngine:
         ch.loss = loss.data_ptr()
         _lib.check(L.drpo_critic_head(ctypes.byref(ch), _lib.stream()), 'critic_head')
         # backward: critics (twin) and constraint critic (trunk + heads)
-        self._run_bwd('c.bq', lambda: fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B))
         heads = [n['cc_trunk'], n['cc_mean']] + ([n['cc_ls']] if dist else [])
-        self._run_bwd('c.bcc' + str(int(dist)), lambda: fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)],
-                                                                 B, trunk=True))
+        self._run_bwd_multi('c.b' + str(int(dist)), lambda: [
+            fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B),
+            fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)], B, trunk=True)])
         tsy = n['cc_trunk'].sy
         items = [(n['q0'], [xs, n['q0'].sy[0], n['q0'].sy[1]]), (n['q1'], [xs, n['q1'].sy[0], n['q1'].sy[1]]),
                  (n['cc_trunk'], [xs, tsy[0]]), (n['cc_mean'], [tsy[-1], n['cc_mean'].sy[0]])]
@@ -492,26 +536,25 @@ class SACEngine:
             noise.randn_like(qshape, used=False)
         ctr = noise.next()
         cc = sol.constraint_critic
-        # actor rsample with saves
-        xa = self.buf('a.x', B, S)
-        self._run_fwd('a.actor', lambda: fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa))
-        raw = n['actor'].sy[-1]
+        xa, xs = self.buf('a.x', B, S), self.buf('a.xs', B, S)
         a, lp, u, e = self.buf('a.a', B, A), self.buf('a.lp', B), self.buf('a.u', B, A), self.buf('a.e', B, A)
-        self._policy_head(raw, 1, e5, SITE_PI_RS, ctr, a=a, logp=lp, u=u, e=e)
-        qk = n['q0'] if k == 0 else n['q1']
-        self._run_fwd(f'a.q{k}', lambda: fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B))
-        self._run_fwd('a.cc', lambda: fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B,
-                                               trunk=True))
-        # safe actor (rsample + its mean action)
-        xs = self.buf('a.xs', B, S)
-        self._run_fwd('a.safe', lambda: fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xs))
-        raws = n['safe'].sy[-1]
         a_s, u_s, e_s, am = self.buf('a.as', B, A), self.buf('a.us', B, A), self.buf('a.es', B, A), \
             self.buf('a.am', B, A)
-        self._policy_head(raws, 1, e6, SITE_SAFE_RS, ctr, a=a_s, u=u_s, e=e_s, amean=am)
+        raw, raws = n['actor'].sy[-1], n['safe'].sy[-1]
+        # launch 1: actor and safe actor rsample (saves for backward) + fused heads
+        self._run_multi('a.f1' + noise_tag(e5), lambda: [
+            with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE, A,
+                      e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e),
+            with_head(fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xs), HEAD_RSAMPLE, A,
+                      e6, SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am)], ctr)
+        # launch 2: Q_k(s, a), Qc(s, a), Qc(s, a_safe) with saves; Qc(s, tanh(mu_safe)) for lam
+        qk = n['q0'] if k == 0 else n['q1']
+        self._run_multi(f'a.f2.{k}', lambda: [
+            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B),
+            fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
+            fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True),
+            fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True)], ctr)
         # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad)
-        self._run_fwd('a.ccm', lambda: fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B,
-                                                trunk=True))
         sqc = self.buf('a.sqc', B)
         self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
         self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
@@ -519,9 +562,6 @@ class SACEngine:
         lams = self.buf('a.lams', B)
         _lib.check(L.drpo_multiplier_out(B, ws['a.multx'].data_ptr(), float(sol.mlp_multiplier_cfg.upper_bound),
                                          lams.data_ptr(), _lib.stream()), 'multiplier_out')
-        # constraint critic at (s, a_safe) with saves
-        self._run_fwd('a.cc2', lambda: fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B,
-                                                trunk=True))
         # upstream gradients
         ca, cs = self._cc_views('a.cc'), self._cc_views('a.cc2')
         gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
@@ -531,28 +571,29 @@ class SACEngine:
                                          cs[0].data_ptr(), cs[1].data_ptr(), gq.data_ptr(), gmu.data_ptr(),
                                          gls.data_ptr(), gmu2.data_ptr(), gls2.data_ptr(), _lib.stream()),
                    'actor_upstream')
-        dA, dAs = self.buf('a.dA', B, A), self.buf('a.dAs', B, A)
-        self._run_bwd(f'a.bq{k}', lambda: fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)}))
-        hv = self.nets_view['a.cc']
-        self._run_bwd('a.bcc', lambda: fill_bwd(hv if dist else hv[:2], [None, gmu, gls][:3 if dist else 2], B,
-                                                trunk=True, dx={0: (dA, S, A, True)}))
-        hv2 = self.nets_view['a.cc2']
-        self._run_bwd('a.bcc2', lambda: fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B,
-                                                 trunk=True, dx={0: (dAs, S, A, False)}))
+        # dL/da of the actor (Q_k part + certificate part, summed in squash_backward in
+        # the reference's order) and of the safe actor: one backward launch
+        dA, dAc, dAs = self.buf('a.dA', B, A), self.buf('a.dAc', B, A), self.buf('a.dAs', B, A)
+        hv, hv2 = self.nets_view['a.cc'], self.nets_view['a.cc2']
+        self._run_bwd_multi(f'a.b.{k}{int(dist)}', lambda: [
+            fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)}),
+            fill_bwd(hv if dist else hv[:2], [None, gmu, gls][:3 if dist else 2], B, trunk=True,
+                     dx={0: (dAc, S, A, False)}),
+            fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B, trunk=True,
+                     dx={0: (dAs, S, A, False)})])
         # squashed Gaussian backward -> actor heads; alpha loss sum
         asum = self._loss_slots(1)
         draw, draws = self.buf('a.draw', B, 2 * A), self.buf('a.draws', B, 2 * A)
         _lib.check(L.drpo_squash_backward(B, A, raw.data_ptr(), u.data_ptr(), e.data_ptr(), dA.data_ptr(),
-                                          sol.log_alpha.data_ptr(), 1.0 / B, lp.data_ptr(),
+                                          dAc.data_ptr(), sol.log_alpha.data_ptr(), 1.0 / B, lp.data_ptr(),
                                           float(sol.target_entropy), asum.data_ptr(), draw.data_ptr(),
                                           _lib.stream()), 'squash_backward')
         _lib.check(L.drpo_squash_backward(B, A, raws.data_ptr(), u_s.data_ptr(), e_s.data_ptr(), dAs.data_ptr(),
-                                          None, 0.0, None, 0.0, None, draws.data_ptr(), _lib.stream()),
+                                          None, None, 0.0, None, 0.0, None, draws.data_ptr(), _lib.stream()),
                    'squash_backward_safe')
         self._clean_grads(sol.actor.group)
         self._clean_grads(sol.actor_safe.group)
-        self._run_bwd('a.bact', lambda: fill_bwd([n['actor']], [draw], B))
-        self._run_bwd('a.bsafe', lambda: fill_bwd([n['safe']], [draws], B))
+        self._run_bwd_multi('a.bpi', lambda: [fill_bwd([n['actor']], [draw], B), fill_bwd([n['safe']], [draws], B)])
         na, ns = n['actor'], n['safe']
         self._run_wgrad('a.wg', lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]]), (ns, [xs, ns.sy[0], ns.sy[1]])],
                                                     B))
@@ -636,21 +677,19 @@ class SACEngine:
             noise.randn_like(qshape, used=False)
             noise.randn_like(qshape, used=False)
         ctr = noise.next()
-        self._run_fwd('m.actor', lambda: fill_fwd([self._out_net(n['actor'], 'm.raw', B)],
-                                                  [(self.bs, S), (None, 0), (None, 0)], B))
-        a = self.buf('m.a', B, A)
-        self._policy_head(ws['m.raw'], 1, e7, SITE_PI_MULT, ctr, a=a)
-        self._run_fwd('m.cc', lambda: fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B,
-                                               trunk=True))
-        aqc = self.buf('m.aqc', B)
+        a, am = self.buf('m.a', B, A), self.buf('m.am', B, A)
+        # launch 1: a ~ pi(s) (rsample) and tanh(mu_safe(s)) via fused heads
+        self._run_multi('m.f1' + noise_tag(e7), lambda: [
+            with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A,
+                      e7, SITE_PI_MULT, a=a),
+            with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A, None,
+                      0, amean=am)], ctr)
+        # launch 2: constraint critic at (s, a) and at (s, tanh(mu_safe))
+        self._run_multi('m.f2', lambda: [
+            fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
+            fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True)], ctr)
+        aqc, sqc = self.buf('m.aqc', B), self.buf('m.sqc', B)
         self._cc_head(ws['m.cc.mu'], ws['m.cc.ls'], aqc, dist)
-        self._run_fwd('m.safe', lambda: fill_fwd([self._out_net(n['safe'], 'm.raws', B)],
-                                                 [(self.bs, S), (None, 0), (None, 0)], B))
-        am = self.buf('m.am', B, A)
-        self._policy_head(ws['m.raws'], 2, None, 0, ctr, amean=am)
-        self._run_fwd('m.ccs', lambda: fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B,
-                                                trunk=True))
-        sqc = self.buf('m.sqc', B)
         self._cc_head(ws['m.ccs.mu'], ws['m.ccs.ls'], sqc, dist)
         xm = self.buf('m.x', B, S + 1)
         self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B, save_x=xm))
