@@ -533,6 +533,7 @@ struct WgradArgs {
   drpo_wgrad_item_t it[WG_MAXITEMS];
   int64_t first[WG_MAXITEMS + 1];
   int n;
+  int chunk;                        // rows per workgroup (multiple of WG_STAGE)
 };
 
 // rows [r, r+1) x 64 columns [c0, c0+64) of a row-major [rows][ld] matrix -> 16 floats
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
   int64_t loc = bid - a.first[q];
   const int ti = (I.din + WG_T - 1) / WG_T;
   const int to = (I.dout + WG_T - 1) / WG_T;
-  const int nch = (int)((I.rows + WG_CHUNK - 1) / WG_CHUNK);
+  const int nch = (int)((I.rows + a.chunk - 1) / a.chunk);
   const int ch = (int)(loc % nch); loc /= nch;
   const int it_i = (int)(loc % ti); loc /= ti;
   const int it_o = (int)(loc % to); loc /= to;
@@ -567,8 +568,8 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
   const float* dz = I.dz + (size_t)zb * I.zstride;
   const float* y = I.y + (size_t)zb * I.ystride;
   const int o0 = it_o * WG_T, i0 = it_i * WG_T;
-  const int64_t r0 = (int64_t)ch * WG_CHUNK;
-  const int64_t r1 = min(I.rows, r0 + WG_CHUNK);
+  const int64_t r0 = (int64_t)ch * a.chunk;
+  const int64_t r1 = min(I.rows, r0 + a.chunk);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -672,6 +673,20 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS, "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
   WgradArgs a{};
+  // split-K over the batch: largest row chunk that still gives >= 2 workgroups per CU
+  // (fewer rows per chunk means more float atomics into the flat gradient)
+  auto count = [&](int chunk) {
+    int64_t t = 0;
+    for (int k = 0; k < n; ++k) {
+      const drpo_wgrad_item_t& I = items[k];
+      if (I.rows <= 0) continue;
+      t += (int64_t)((I.din + WG_T - 1) / WG_T) * ((I.dout + WG_T - 1) / WG_T) * ((I.rows + chunk - 1) / chunk) *
+           I.nbatch;
+    }
+    return t;
+  };
+  a.chunk = WG_CHUNK;
+  while (a.chunk > WG_STAGE * 4 && count(a.chunk) < 384) a.chunk >>= 1;
   int64_t tot = 0;
   int m = 0;
   for (int k = 0; k < n; ++k) {
@@ -682,7 +697,7 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t
     a.it[m] = I;
     a.first[m] = tot;
     const int64_t ti = (I.din + WG_T - 1) / WG_T, to = (I.dout + WG_T - 1) / WG_T;
-    tot += ti * to * ((I.rows + WG_CHUNK - 1) / WG_CHUNK) * I.nbatch;
+    tot += ti * to * ((I.rows + a.chunk - 1) / a.chunk) * I.nbatch;
     ++m;
   }
   a.first[m] = tot;

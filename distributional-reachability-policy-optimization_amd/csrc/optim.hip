@@ -12,7 +12,7 @@
 
 using namespace drpo;
 
-static constexpr int SUMSQ_BLOCK_ELEMS = 8192;
+static constexpr int SUMSQ_BLOCK_ELEMS = 2048;
 
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, float* partial) {
   __shared__ float red[256];

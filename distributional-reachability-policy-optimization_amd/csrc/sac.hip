@@ -80,21 +80,26 @@ __global__ void sample_batch_kernel(drpo_buffer_view_t real, drpo_buffer_view_t 
                             (uint32_t)(seed >> 32));
     q = (int64_t)(((uint64_t)rr.x * (uint64_t)len) >> 32);
   }
-  for (int k = 0; k < S; ++k) {
-    os[(int64_t)i * S + k] = bv.s[q * S + k];
-    os2[(int64_t)i * S + k] = bv.s2[q * S + k];
-  }
-  for (int k = 0; k < A; ++k) oa[(int64_t)i * A + k] = bv.a[q * A + k];
-  float r = bv.r[q];
-  if (reward_scale != 0.f) r = r * reward_scale;
-  if (alive_bonus != 0.f) r = r + alive_bonus;
-  orw[i] = r;
-  od[i] = bv.d[q];
-  ov[i] = bv.v[q];
-  for (int c = 0; c < C; ++c) {
-    float hv = bv.h[q * C + c] * cscale;
-    hv = hv + (hv > 0.f ? 1.f : 0.f) * coffset;
-    oh[(int64_t)i * C + c] = hv;
+  // grid.y splits the row's components over 4 threads (more loads in flight)
+  const int part = blockIdx.y;
+  if (part == 0) {
+    for (int k = 0; k < S; ++k) os[(int64_t)i * S + k] = bv.s[q * S + k];
+  } else if (part == 1) {
+    for (int k = 0; k < S; ++k) os2[(int64_t)i * S + k] = bv.s2[q * S + k];
+  } else if (part == 2) {
+    for (int k = 0; k < A; ++k) oa[(int64_t)i * A + k] = bv.a[q * A + k];
+    float r = bv.r[q];
+    if (reward_scale != 0.f) r = r * reward_scale;
+    if (alive_bonus != 0.f) r = r + alive_bonus;
+    orw[i] = r;
+    od[i] = bv.d[q];
+    ov[i] = bv.v[q];
+  } else {
+    for (int c = 0; c < C; ++c) {
+      float hv = bv.h[q * C + c] * cscale;
+      hv = hv + (hv > 0.f ? 1.f : 0.f) * coffset;
+      oh[(int64_t)i * C + c] = hv;
+    }
   }
 }
 
@@ -106,7 +111,7 @@ DRPO_API int drpo_sample_batch(const drpo_buffer_view_t* real, const drpo_buffer
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(real && virt && B >= 0 && n_real >= 0 && n_real <= B, "drpo_sample_batch: bad sizes");
   if (B == 0) return DRPO_OK;
-  sample_batch_kernel<<<(B + 255) / 256, 256, 0, stream>>>(*real, *virt, n_real, B, S, A, C, idx_real, idx_virt, seed,
+  sample_batch_kernel<<<dim3((B + 63) / 64, 4), 64, 0, stream>>>(*real, *virt, n_real, B, S, A, C, idx_real, idx_virt, seed,
                                                           ctr, reward_scale, alive_bonus, constraint_scale,
                                                           constraint_offset, s, a, s2, r, d, v, h);
   DRPO_LAUNCH_CHECK("sample_batch");
@@ -144,7 +149,7 @@ DRPO_API int drpo_policy_head(const float* raw, int64_t B, int A, int mode, cons
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(mode >= 0 && mode <= 3 && A >= 1, "drpo_policy_head: bad mode/A");
   if (B == 0) return DRPO_OK;
-  policy_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(raw, B, A, mode, eps, seed, ctr, site, a, logp,
+  policy_head_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(raw, B, A, mode, eps, seed, ctr, site, a, logp,
                                                                       u, e, amean);
   DRPO_LAUNCH_CHECK("policy_head");
   return DRPO_OK;
@@ -172,7 +177,7 @@ DRPO_API int drpo_cc_head(const float* mu, const float* lsraw, int64_t B, int C,
                           float log_std_min, float log_std_max, float* ubmax, int* argmax, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
-  cc_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(mu, lsraw, B, C, distributional, std_ratio,
+  cc_head_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(mu, lsraw, B, C, distributional, std_ratio,
                                                                   log_std_min, log_std_max, ubmax, argmax);
   DRPO_LAUNCH_CHECK("cc_head");
   return DRPO_OK;
@@ -275,7 +280,7 @@ DRPO_API int drpo_critic_head(const drpo_critic_head_t* p, drpo_stream_t stream_
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(p && p->C >= 1 && p->B >= 0, "drpo_critic_head: bad descriptor");
   if (p->B == 0) return DRPO_OK;
-  critic_head_kernel<<<(unsigned)((p->B + 255) / 256), 256, 0, stream>>>(*p);
+  critic_head_kernel<<<(unsigned)((p->B + 63) / 64), 64, 0, stream>>>(*p);
   DRPO_LAUNCH_CHECK("critic_head");
   return DRPO_OK;
 }
@@ -330,7 +335,7 @@ DRPO_API int drpo_actor_upstream(int64_t B, int C, int distributional, float std
                                  float* gmu_s, float* gls_s, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
-  actor_upstream_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(
+  actor_upstream_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(
       B, C, distributional, std_ratio, log_std_min, log_std_max, lams, mu_a, ls_a, mu_s, ls_s, gq, gmu_a, gls_a,
       gmu_s, gls_s);
   DRPO_LAUNCH_CHECK("actor_upstream");
@@ -381,7 +386,7 @@ DRPO_API int drpo_squash_backward(int64_t B, int A, const float* raw, const floa
                                   float* alpha_sum, float* draw, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
-  squash_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(B, A, raw, u, e, dA, dA2, log_alpha, lp_scale, logp,
+  squash_bwd_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(B, A, raw, u, e, dA, dA2, log_alpha, lp_scale, logp,
                                                                      target_entropy, alpha_sum, draw);
   DRPO_LAUNCH_CHECK("squash_backward");
   return DRPO_OK;
@@ -432,7 +437,7 @@ DRPO_API int drpo_multiplier_head(int64_t B, const float* x, const float* safe_q
                                   float lam_epsilon, float* gx, float* loss, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
-  multiplier_head_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(
+  multiplier_head_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(
       B, x, safe_qc, actor_qc, threshold, penalty_lb, penalty_ub, upper_bound, lam_epsilon, gx, loss);
   DRPO_LAUNCH_CHECK("multiplier_head");
   return DRPO_OK;
@@ -447,7 +452,7 @@ __global__ void multiplier_out_kernel(int64_t B, const float* x, float ub, float
 DRPO_API int drpo_multiplier_out(int64_t B, const float* x, float upper_bound, float* lam, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
-  multiplier_out_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(B, x, upper_bound, lam);
+  multiplier_out_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(B, x, upper_bound, lam);
   DRPO_LAUNCH_CHECK("multiplier_out");
   return DRPO_OK;
 }

@@ -433,17 +433,19 @@ class SACEngine:
         a2, lp2, a2s = self.buf('c.a2', B, A), self.buf('c.lp2', B), self.buf('c.a2s', B, A)
         # launch 1: a' ~ pi(s') with log pi, a'_safe ~ pi_safe(s') (robust: model s'), and
         # the twin critics + constraint critic at (s, a) with their backward saves
+        # (jobs are ordered longest chain first: workgroups dispatch in slot order, so the
+        # short chains fill the tail instead of leaving the long ones running alone)
         self._run_multi('c.f1' + rk + noise_tag(e1), lambda: [
+            fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
+            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs),
             with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs2, S), (None, 0), (None, 0)], B), HEAD_SAMPLE, A,
                       e1, SITE_PI_NEXT, a=a2, logp=lp2),
             with_head(fill_fwd([Net(n['safe'].layers)], [(s2c, S), (None, 0), (None, 0)], B), HEAD_SAMPLE, A, e2,
-                      SITE_SAFE_NEXT, a=a2s),
-            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs),
-            fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True)], ctr)
-        # launch 2: target critics at (s', a') and target constraint critic at (s', a'_safe)
+                      SITE_SAFE_NEXT, a=a2s)], ctr)
+        # launch 2: target constraint critic at (s', a'_safe) and target critics at (s', a')
         self._run_multi('c.f2' + rk, lambda: [
-            fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (a2, A), (None, 0)], B),
-            fill_fwd(self._cc_nets('t'), [(s2c, S), (a2s, A), (None, 0)], B, trunk=True)], ctr)
+            fill_fwd(self._cc_nets('t'), [(s2c, S), (a2s, A), (None, 0)], B, trunk=True),
+            fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (a2, A), (None, 0)], B)], ctr)
         loss = self._loss_slots(2)
         self._clean_grads(sol.critic_group)
         ch = self.desc.get('c.head')
@@ -470,8 +472,8 @@ class SACEngine:
         # backward: critics (twin) and constraint critic (trunk + heads)
         heads = [n['cc_trunk'], n['cc_mean']] + ([n['cc_ls']] if dist else [])
         self._run_bwd_multi('c.b' + str(int(dist)), lambda: [
-            fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B),
-            fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)], B, trunk=True)])
+            fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)], B, trunk=True),
+            fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B)])
         tsy = n['cc_trunk'].sy
         items = [(n['q0'], [xs, n['q0'].sy[0], n['q0'].sy[1]]), (n['q1'], [xs, n['q1'].sy[0], n['q1'].sy[1]]),
                  (n['cc_trunk'], [xs, tsy[0]]), (n['cc_mean'], [tsy[-1], n['cc_mean'].sy[0]])]
@@ -550,10 +552,10 @@ class SACEngine:
         # launch 2: Q_k(s, a), Qc(s, a), Qc(s, a_safe) with saves; Qc(s, tanh(mu_safe)) for lam
         qk = n['q0'] if k == 0 else n['q1']
         self._run_multi(f'a.f2.{k}', lambda: [
-            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B),
             fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
             fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True),
-            fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True)], ctr)
+            fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True),
+            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)], ctr)
         # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad)
         sqc = self.buf('a.sqc', B)
         self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
@@ -576,11 +578,11 @@ class SACEngine:
         dA, dAc, dAs = self.buf('a.dA', B, A), self.buf('a.dAc', B, A), self.buf('a.dAs', B, A)
         hv, hv2 = self.nets_view['a.cc'], self.nets_view['a.cc2']
         self._run_bwd_multi(f'a.b.{k}{int(dist)}', lambda: [
-            fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)}),
             fill_bwd(hv if dist else hv[:2], [None, gmu, gls][:3 if dist else 2], B, trunk=True,
                      dx={0: (dAc, S, A, False)}),
             fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B, trunk=True,
-                     dx={0: (dAs, S, A, False)})])
+                     dx={0: (dAs, S, A, False)}),
+            fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)})])
         # squashed Gaussian backward -> actor heads; alpha loss sum
         asum = self._loss_slots(1)
         draw, draws = self.buf('a.draw', B, 2 * A), self.buf('a.draws', B, 2 * A)
