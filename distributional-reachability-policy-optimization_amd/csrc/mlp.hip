@@ -53,15 +53,18 @@ DRPO_API int drpo_debug_stamps(unsigned long long* dst, int n) {
   do {           \
   } while (0)
 #endif
-template <int ACT>
+template <int ACT, int RB>
 __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const drpo_mlp_layer_t& L, const float* W,
                                               const float* b, float* out, int ldo, float* red, const GSave& gs) {
   if (L.dout <= 16)
-    tile_dense_narrow<FW_NW, 1, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, red, gs);
+    tile_dense_narrow<FW_NW, RB, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, red, gs);
   else
-    tile_dense<FW_NW, 1, FW_MAXC, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, gs);
+    tile_dense<FW_NW, RB, FW_MAXC, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, gs);
 }
 
+// one layer of a (16*RB)-row tile: packed weights of batch item z, bias, activation,
+// optional global saves of the post-/pre-activation for the backward pass
+template <int RB = 1>
 __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& __restrict__ L, int z, int64_t rows,
                                           int row0, int nrows, float* out, float* red) {
   const float* W = L.W + (size_t)z * L.wstride;
@@ -69,10 +72,10 @@ __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_m
   const size_t so = ((size_t)z * rows + row0) * L.dout;
   GSave gs{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
   switch (L.act) {
-    case ACT_RELU: run_layer_act<ACT_RELU>(in, LDH, L, W, b, out, LDH, red, gs); break;
-    case ACT_SILU: run_layer_act<ACT_SILU>(in, LDH, L, W, b, out, LDH, red, gs); break;
-    case ACT_TANH: run_layer_act<ACT_TANH>(in, LDH, L, W, b, out, LDH, red, gs); break;
-    default: run_layer_act<ACT_NONE>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_RELU: run_layer_act<ACT_RELU, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_SILU: run_layer_act<ACT_SILU, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_TANH: run_layer_act<ACT_TANH, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    default: run_layer_act<ACT_NONE, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
   }
   (void)ldi;
 }
@@ -184,37 +187,40 @@ struct MultiArgs {
   uint64_t seed, ctr;
 };
 
+template <int RB>
 __device__ __forceinline__ float* run_net_g(const drpo_mlp_fwd_t* __restrict__ a, int ni, float* in, float* bufA,
                                             float* bufB, int z, int row0, int nrows, float* red) {
   float* cur = in;
   const int nl = a->net[ni].nl;
   for (int l = 0; l < nl; ++l) {
     float* out = (cur == bufA) ? bufB : bufA;
-    run_layer(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
+    run_layer<RB>(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
     __syncthreads();
     cur = out;
   }
   return cur;
 }
 
-__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_fwd_multi_kernel(MultiArgs m) {
+template <int RB>
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ? 4 : 2, RB == 1 ? 4 : 2))) void mlp_fwd_multi_kernel(MultiArgs m) {
+  constexpr int ROWS = 16 * RB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xin = smem;
-  float* bA = xin + FW_ROWS * LDH;
-  float* bB = bA + FW_ROWS * LDH;
-  float* T = bB + FW_ROWS * LDH;
-  float* red = T + FW_ROWS * LDH;
+  float* bA = xin + ROWS * LDH;
+  float* bB = bA + ROWS * LDH;
+  float* T = bB + ROWS * LDH;
+  float* red = T + ROWS * LDH;
   const drpo_mlp_fwd_t* __restrict__ a = m.jobs + m.slot_job[blockIdx.y];
   const int net = m.slot_net[blockIdx.y];
   const int tid = threadIdx.x;
   const int z = blockIdx.z;
-  const int row0 = blockIdx.x * FW_ROWS;
+  const int row0 = blockIdx.x * ROWS;
   if (row0 >= a->rows || z >= a->nbatch) return;
-  const int nrows = (int)min((int64_t)FW_ROWS, a->rows - row0);
+  const int nrows = (int)min((int64_t)ROWS, a->rows - row0);
   const int c0 = a->cols[0], c1 = a->cols[1];
   const int din0 = c0 + c1 + a->cols[2];
   const int kpad = round_up(din0, 16);
-  for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
+  for (int e = tid; e < ROWS * kpad; e += FW_NT) {
     const int r = e / kpad, k = e - r * kpad;
     float v = 0.f;
     if (r < nrows && k < din0) {
@@ -230,18 +236,18 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __syncthreads();
   float* outp;
   if (!a->trunk) {
-    outp = run_net_g(a, net, xin, bA, bB, z, row0, nrows, red);
+    outp = run_net_g<RB>(a, net, xin, bA, bB, z, row0, nrows, red);
   } else {
-    float* t = run_net_g(a, 0, xin, bA, bB, z, row0, nrows, red);
+    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
     const int w = a->net[0].L[a->net[0].nl - 1].dout;
     const int wpad = round_up(w, 16);
-    for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
+    for (int e = tid; e < ROWS * wpad; e += FW_NT) {
       const int r = e / wpad, k = e - r * wpad;
       T[r * LDH + k] = t[r * LDH + k];
     }
     __syncthreads();
     outp = nullptr;
-    for (int h = 1; h < a->nnets; ++h) run_net_g(a, h, T, bA, bB, z, row0, nrows, red);
+    for (int h = 1; h < a->nnets; ++h) run_net_g<RB>(a, h, T, bA, bB, z, row0, nrows, red);
   }
   // fused squashed-Gaussian head on net 0's output (non-trunk jobs)
   const drpo_policy_head_t& hd = a->head;
@@ -292,7 +298,15 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
     nbatch = max(nbatch, a->nbatch);
   }
   if (tiles == 0) return DRPO_OK;
-  mlp_fwd_multi_kernel<<<dim3((unsigned)tiles, slots, nbatch), FW_NT, fwd_lds(), stream>>>(m);
+  // 32-row tiles halve the weight bytes per MFMA but allow only one 8-wave workgroup
+  // per CU (LDS); measured slower at B=4096 (profiles/r01), so only for launches
+  // with >= 8 workgroups per CU at 16-row tiles
+  if (tiles * slots * nbatch >= 2048) {
+    const size_t lds = sizeof(float) * ((size_t)4 * 2 * FW_ROWS * LDH + FW_NW * 2 * 256);
+    mlp_fwd_multi_kernel<2><<<dim3((unsigned)((tiles + 1) / 2), slots, nbatch), FW_NT, lds, stream>>>(m);
+  } else {
+    mlp_fwd_multi_kernel<1><<<dim3((unsigned)tiles, slots, nbatch), FW_NT, fwd_lds(), stream>>>(m);
+  }
   DRPO_LAUNCH_CHECK("mlp_forward_multi");
   return DRPO_OK;
 }
