@@ -241,6 +241,22 @@ def main():
     else:
         wall, roll_s, sac_s, n_all = tot[0].item(), tot[1].item(), tot[2].item(), tot[3].item()
 
+    # post-pass (untimed): per-kernel-class MLP throughput of the SAC update from HIP
+    # events around every MLP launch (drpo_amd.sac_step.LaunchProfiler)
+    sac_kernels = None
+    if do_sac and rank == 0:
+        from drpo_amd.sac_step import LaunchProfiler
+        eng = alg.solver.engine
+        eng.profiler = LaunchProfiler()
+        for st in range(alg.solver_updates_per_step):
+            alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
+        torch.cuda.synchronize()
+        summ = eng.profiler.summarise()
+        eng.profiler = None
+        sac_kernels = {k: {'tflops': round(v['tflops'], 2), 'frac': round(v['tflops'] / FP32_PEAK_TFLOPS, 4),
+                           'avg_launch_us': round(v['avg_ms'] * 1e3, 2), 'launches': v['launches']}
+                       for k, v in summ.items() if ':' not in k}
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -266,7 +282,10 @@ def main():
                 if do_sac and sac_s > 0 else None,
                 'global_batch': B * world, 'gradient_exchange': 'RCCL all-reduce (mean) per optimizer group'
                 if world > 1 else None,
-                'flop_per_step': sac_flop_per_step(B), 'measured': do_sac},
+                'flop_per_step': sac_flop_per_step(B), 'measured': do_sac,
+                'achieved_tflops_per_gpu': (sac_flop_per_step(B) * alg.solver_updates_per_step * args.steps / sac_s / 1e12)
+                if do_sac and sac_s > 0 else None,
+                'mlp_kernels': sac_kernels},
         'roofline': {'kernel': 'rollout_step_kernel', 'bound': 'mfma', 'achieved': achieved,
                      'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_PEAK_TFLOPS,
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,
