@@ -227,18 +227,19 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
 // ring and the one-step-ahead LDS A prefetch are indexed statically and the
 // compiler's vmcnt accounting never has to cross a loop back-edge (a back-edge
 // forces vmcnt(0), collapsing the prefetch distance). NK == 0: runtime K loop.
+// Core of tile_dense_impl for a wave that owns exactly MAXC valid column blocks
+// (the dispatcher below picks the instantiation per wave).
 template <int NW, int RB, int MAXC, int ACT, int NK>
-__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ P,
+__device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,
-                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+                                                const GSave& gs) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
   const int NKS = NK > 0 ? NK : (K + 15) >> 4;
-  const int NCB = (N + 15) >> 4;
   int cbs[MAXC];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) cbs[c] = min(wave + NW * c, NCB - 1);
+  for (int c = 0; c < MAXC; ++c) cbs[c] = wave + NW * c;
 
   f32x4 acc[RB][MAXC];
 #pragma unroll
@@ -307,6 +308,28 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
     }
   }
   dense_epilogue<NW, RB, MAXC, ACT>(acc, bvs, N, out, ldo, gs);
+}
+
+// Wave w owns column blocks w, w+NW, ... < NCB: when NW does not divide NCB (13
+// blocks of a 200-wide layer on 8 waves) the waves own different counts, and each
+// runs the instantiation for its own count, so no wave loads or multiplies a
+// padding block (the branch is wave-uniform).
+template <int NW, int RB, int NC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_nc(int nc, const float* in, int ldi, int K, const float* __restrict__ P,
+                                              const float* __restrict__ bias, int N, float* out, int ldo,
+                                              const GSave& gs) {
+  if (nc == NC) tile_dense_core<NW, RB, NC, ACT, NK>(in, ldi, K, P, bias, N, out, ldo, gs);
+  else if constexpr (NC > 1) tile_dense_nc<NW, RB, NC - 1, ACT, NK>(nc, in, ldi, K, P, bias, N, out, ldo, gs);
+}
+
+template <int NW, int RB, int MAXC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ P,
+                                                const float* __restrict__ bias, int N, float* out, int ldo,
+                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NCB = (N + 15) >> 4;
+  const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
+  tile_dense_nc<NW, RB, MAXC, ACT, NK>(nc, in, ldi, K, P, bias, N, out, ldo, gs);
 }
 
 // K (input width) -> compile-time k-step count for the widths on the path
@@ -398,10 +421,10 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
 // (N2 -> out2). One pass instead of two halves the layer's serial latency and
 // gives each wave more independent accumulators.
 template <int NW, int RB, int MAXC, int ACT, int NK>
-__device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K, const float* __restrict__ P1,
-                                                const float* __restrict__ b1, int N1, float* out1,
-                                                const float* __restrict__ P2, const float* __restrict__ b2, int N2,
-                                                float* out2, int ldo) {
+__device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, int K, const float* __restrict__ P1,
+                                                     const float* __restrict__ b1, int N1, float* out1,
+                                                     const float* __restrict__ P2, const float* __restrict__ b2,
+                                                     int N2, float* out2, int ldo) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -411,7 +434,7 @@ __device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K,
   float bvs[MAXC];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int cb = min(wave + NW * c, NCB1 + NCB2 - 1);
+    const int cb = wave + NW * c;   // < NCB1 + NCB2 (the dispatcher's count)
     const bool second = cb >= NCB1;
     Pc[c] = second ? P2 : P1;
     cbs[c] = second ? cb - NCB1 : cb;
@@ -471,6 +494,26 @@ __device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K,
         out[row * ldo + col] = (col < nn) ? act_fn<ACT>(acc[rb][c][r] + bvs[c]) : 0.f;
       }
   }
+}
+
+template <int NW, int RB, int NC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_pair_nc(int nc, const float* in, int ldi, int K, const float* P1,
+                                                   const float* b1, int N1, float* out1, const float* P2,
+                                                   const float* b2, int N2, float* out2, int ldo) {
+  if (nc == NC) tile_dense_pair_core<NW, RB, NC, ACT, NK>(in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
+  else if constexpr (NC > 1)
+    tile_dense_pair_nc<NW, RB, NC - 1, ACT, NK>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
+}
+
+// per-wave block count dispatch as in tile_dense_impl
+template <int NW, int RB, int MAXC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K, const float* P1, const float* b1,
+                                                int N1, float* out1, const float* P2, const float* b2, int N2,
+                                                float* out2, int ldo) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NCB = ((N1 + 15) >> 4) + ((N2 + 15) >> 4);
+  const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
+  tile_dense_pair_nc<NW, RB, MAXC, ACT, NK>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
 }
 
 // Two narrow layers (N1, N2 <= 16) on two input tiles at once: waves [0, NW/2) split
