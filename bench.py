@@ -161,6 +161,7 @@ def main():
     ap.add_argument('--rollout-only', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--engine', type=int, default=0, help='rollout engine: 0 auto (fused horizon), 1 per-step launches')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -178,6 +179,7 @@ def main():
     import drpo_amd
     from drpo_amd.ops import EventTimer
     alg = make_alg(dev, B, H, E, args.seed + rank, QUAD_JSON)
+    alg.rollout_engine = args.engine
     rep = synth_replay(12, 2, 2, 100000, np.random.RandomState(args.seed + rank))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
@@ -229,7 +231,7 @@ def main():
     for e, tmr in zip(evs, timers):
         roll_ms.append(e[0].elapsed_time(e[1]))
         sac_ms.append(e[1].elapsed_time(e[2]))
-        kern_ms.extend(tmr.elapsed_pairs(H))
+        kern_ms.extend(tmr.elapsed_pairs(getattr(tmr, 'pairs', H)))
     n_trans = int(n_dev.item())
     tot = torch.tensor([wall, sum(roll_ms) / 1e3, sum(sac_ms) / 1e3, float(n_trans)], dtype=torch.float64, device=dev)
     if dist is not None:
@@ -262,6 +264,8 @@ def main():
             dist.destroy_process_group()
         return
     flop_tr = rollout_flop_per_transition(12, 2)
+    fused = getattr(timers[0], 'pairs', H) == 1
+    kname = 'rollout_persist_kernel' if fused else 'rollout_step_kernel'
     k_avg_ms = float(np.mean(kern_ms))
     rows_per_launch = n_trans / max(1, len(kern_ms))
     achieved = flop_tr * rows_per_launch / (k_avg_ms * 1e-3) / 1e12
@@ -286,14 +290,16 @@ def main():
                 'achieved_tflops_per_gpu': (sac_flop_per_step(B) * alg.solver_updates_per_step * args.steps / sac_s / 1e12)
                 if do_sac and sac_s > 0 else None,
                 'mlp_kernels': sac_kernels},
-        'roofline': {'kernel': 'rollout_step_kernel', 'bound': 'mfma', 'achieved': achieved,
+        'roofline': {'kernel': kname, 'bound': 'mfma', 'achieved': achieved,
                      'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_PEAK_TFLOPS,
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,
                      'rows_per_launch': rows_per_launch},
     }
-    prof = os.path.join(ROOT, 'profiles', 'traffic_rollout_step.json')
+    prof = os.path.join(ROOT, 'profiles', 'traffic_rollout_fused.json' if fused else 'traffic_rollout_step.json')
     if os.path.exists(prof):
-        res['roofline']['traffic'] = json.load(open(prof)).get('bytes_per_launch')
+        tr = json.load(open(prof))
+        if tr.get('kernel') == kname:
+            res['roofline']['traffic'] = tr.get('bytes_per_launch')
     if world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(B, H, E, args.seed)
     print(json.dumps(res))

@@ -25,6 +25,7 @@ class RolloutDesc(ctypes.Structure):
         ('vs', P), ('va', P), ('vs2', P), ('vr', P), ('vh', P), ('vd', P), ('vv', P),
         ('vptr', P), ('vcap', c_int64),
         ('workspace', P), ('rows_per_tile', c_int), ('step_events', POINTER(c_void_p)),
+        ('engine', c_int), ('eps_layout', c_int),
     ]
 
 

@@ -159,8 +159,32 @@ __device__ __forceinline__ void squashed_gaussian_row(RawAt raw_at, int64_t i, i
 // backward-data product (dY = dZ W) reads the transposed mirror of the same
 // shape with the roles of N and K exchanged.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ f32x4 load_pk(const float* __restrict__ P, int cb, int s, int NKS) {
-  return *reinterpret_cast<const f32x4*>(P + ((size_t)(cb * NKS + s) << 8) + ((threadIdx.x & 63) << 2));
+//
+// Two address forms, chosen per translation unit. Default: one 64-bit per-lane
+// address per load (fastest for the MLP kernels: the scalar form below measured
+// 5-7% slower there). DRPO_UNIFORM_WEIGHT_LOADS=1 (rollout.hip): (cb, s) are
+// wave-uniform at every call site, so the fragment base is formed in SGPRs and
+// the only per-lane term is the 32-bit lane offset (saddr-form loads). Inside
+// rollout_persist_kernel's horizon loop the per-lane 64-bit addresses are
+// loop-invariant, get hoisted and spill (80 spill slots); the scalar form has none.
+#ifndef DRPO_UNIFORM_WEIGHT_LOADS
+#define DRPO_UNIFORM_WEIGHT_LOADS 0
+#endif
+
+static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
+
+static __device__ __forceinline__ f32x4 load_pk(const float* __restrict__ P, int cb, int s, int NKS) {
+  if constexpr (DRPO_UNIFORM_WEIGHT_LOADS) {
+    const float* base = uniform_ptr(P) + ((size_t)__builtin_amdgcn_readfirstlane(cb * NKS + s) << 8);
+    return *reinterpret_cast<const f32x4*>(base + ((threadIdx.x & 63) << 2));
+  } else {
+    return *reinterpret_cast<const f32x4*>(P + ((size_t)(cb * NKS + s) << 8) + ((threadIdx.x & 63) << 2));
+  }
 }
 
 // Weight fragments are streamed through a static register ring of depth PF_D:
@@ -227,6 +251,20 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
 // ring and the one-step-ahead LDS A prefetch are indexed statically and the
 // compiler's vmcnt accounting never has to cross a loop back-edge (a back-edge
 // forces vmcnt(0), collapsing the prefetch distance). NK == 0: runtime K loop.
+// Workgroup barrier for LDS hand-offs only. __syncthreads() is a workgroup-scope
+// acq_rel fence + s_barrier, and the fence waits for every outstanding global load
+// (vmcnt(0)), which drains weight fragments issued ahead of the barrier. Here each
+// wave waits only for its own LDS traffic (lgkmcnt(0); LDS ops complete in order)
+// before s_barrier (gfx950 backs off barriers with memory operations in flight),
+// and the empty asm with a memory clobber keeps the compiler from moving memory
+// accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Core of tile_dense_impl for a wave that owns exactly MAXC valid column blocks
 // (the dispatcher below picks the instantiation per wave).
 template <int NW, int RB, int MAXC, int ACT, int NK>
@@ -397,7 +435,7 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
-  __syncthreads();
+  lds_barrier();
   for (int e = tid; e < RB * 256; e += NW * 64) {
     const int rb = e >> 8, rr = (e >> 4) & 15, col = e & 15;
     float v = 0.f;
@@ -562,7 +600,7 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
-  __syncthreads();
+  lds_barrier();
   for (int e = tid; e < 2 * RB * 256; e += NW * 64) {
     const int which = e / (RB * 256), e2 = e - which * RB * 256;
     const int rb = e2 >> 8, rr = (e2 >> 4) & 15, col = e2 & 15;

@@ -16,7 +16,9 @@
 // rollout needs no host synchronisation.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
+#define DRPO_UNIFORM_WEIGHT_LOADS 1   // scalar-base weight loads (see load_pk)
 #include "common.hpp"
 #include "env_constraints.hpp"
 
@@ -386,6 +388,397 @@ __global__ void rollout_finalize_kernel(int64_t* vptr, const int* n, int64_t* of
 }
 
 // ---------------------------------------------------------------------------
+// Fused-horizon engine (engine 2). A row's trajectory depends only on its own
+// earlier steps (SMBPO.rollout, src/smbpo.py:229-249: the batch only loses rows),
+// so each workgroup keeps its 16/32-row tile for ALL H steps, with the states in
+// LDS, and no workgroup ever waits for another. Rows that finish (done) stay in
+// the tile masked off. Each step's surviving rows go to a staging area indexed
+// [t][original row] together with per-(t, tile) counts and in-tile maps;
+// rollout_emit_kernel then writes them into the circular buffer in the
+// reference's order (step-major, surviving rows in batch order), which is the
+// order the step engine's compaction produces.
+//
+// Against one launch per step this removes the per-step launch and drain, the
+// device-wide count scan and the binary-searched gather of the previous step's
+// states (bench workload: 37.3 -> 30.9 us per step). The step's Gaussian draws
+// are generated into LDS by waves 1..7 while wave 0 evaluates the previous
+// step's constraints, and the LDS hand-offs use lds_barrier() (no wait on
+// outstanding global loads or the staging stores).
+//
+// Measured and rejected: issuing each layer's first weight k-steps ahead of the
+// barrier / elementwise phase in front of it (and holding the actor's
+// loop-invariant input/output fragments in registers). Across all placements the
+// step time did not change, and the held fragments pushed the kernel to 256 VGPRs
+// with scratch reloads in front of the MFMA loops.
+// ---------------------------------------------------------------------------
+constexpr int PERSIST_MAX_H = 128;
+
+// The actor's weights are the same every step: without this the compiler hoists
+// all of a layer's (restrict, loop-invariant) fragment loads out of the horizon
+// loop and keeps them live in registers for the whole loop (hundreds of spills).
+__device__ __forceinline__ const float* step_opaque(const float* ptr) {
+  asm volatile("" : "+s"(ptr));
+  return ptr;
+}
+
+struct PersistArgs {
+  int S, A, C, Ha, Hm, B, H, ntiles;
+  EnvParams env;
+  const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;
+  // member 0 of the ensemble mirrors / biases; member m adds m * (mstride | bstride)
+  const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2;
+  int64_t ms_in, ms_hid, ms_out;    // packed strides: (S+A -> Hm), (Hm -> Hm), (Hm -> S+1)
+  const float *norm_mean, *norm_std, *min_lv, *max_lv;
+  const float* replay_states;
+  const int64_t* init_idx;
+  int64_t replay_len, replay_ptr, replay_cap;
+  uint32_t prp_key[4];
+  int prp_half_bits;
+  const float* eps_a;   // [H][B][A] original-row layout, or nullptr (Philox)
+  const float* eps_m;   // [H][B][S+1]
+  uint64_t seed, ctr;
+  float *st_s, *st_s2, *st_a, *st_r, *st_h;
+  uint8_t* st_dv;       // bit0 done, bit1 violation
+  int* cnt;             // [H][ntiles] rows alive at the start of step t
+  int* inv;             // [H][ntiles*ROWS] in-tile index of the k-th alive row
+  int ldx, ldh, ldm, lds;
+  int members[PERSIST_MAX_H];
+};
+
+// This step's Gaussian draws into LDS: recorded (original-row layout) or the step
+// engine's Philox keys with the original row. Threads [first, first + count) work.
+template <int ROWS>
+__device__ __forceinline__ void persist_noise(const float* eps_a, const float* eps_m, uint64_t seed, uint64_t ctr,
+                                              int A, int S1, int B, int t, int row0, int nrows, float* nz_a,
+                                              float* nz_m, int first, int count) {
+  const int NA4 = (A + 3) >> 2, NM4 = (S1 + 3) >> 2;
+  const int total = ROWS * (NA4 + NM4);
+  for (int base = 0; base < total; base += count) {   // uniform trip count, divergent body
+    const int i = base + (int)threadIdx.x - first;
+    if (i < base || i >= base + count || i >= total) continue;
+    const int r = i / (NA4 + NM4), q = i - r * (NA4 + NM4);
+    const uint32_t row = (uint32_t)(row0 + r);
+    if (eps_a) {
+      if (q < NA4) {
+        for (int d = 4 * q; d < min(A, 4 * q + 4); ++d)
+          nz_a[r * 8 + d] = r < nrows ? eps_a[((size_t)t * B + row) * A + d] : 0.f;
+      } else {
+        const int q2 = q - NA4;
+        for (int j = 4 * q2; j < min(S1, 4 * q2 + 4); ++j)
+          nz_m[r * 64 + j] = r < nrows ? eps_m[((size_t)t * B + row) * S1 + j] : 0.f;
+      }
+    } else {
+      float z[4];
+      if (q < NA4) {
+        philox_normal4(seed, row, ((uint32_t)t << 8) | 0u, (uint32_t)q, (uint32_t)ctr, z);
+        for (int u = 0; u < 4; ++u) nz_a[r * 8 + 4 * q + u] = z[u];
+      } else {
+        const int q2 = q - NA4;
+        philox_normal4(seed, row, ((uint32_t)t << 8) | 1u, (uint32_t)q2, (uint32_t)ctr, z);
+        for (int u = 0; u < 4; ++u) nz_m[r * 64 + 4 * q2 + u] = z[u];
+      }
+    }
+  }
+}
+
+template <int RB, int NW>
+__global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p) {
+  constexpr int ROWS = RB * 16;
+  constexpr int NT = NW * 64;
+  constexpr int MAXC = (16 + NW - 1) / NW;      // column blocks per wave for widths <= 256
+  constexpr int PMAXC = (32 + NW - 1) / NW;     // paired 200-wide heads: 26 blocks
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int S = p.S, A = p.A, C = p.C, S1 = p.S + 1, B = p.B;
+
+  // LDS carve-up. Re-derived at the top of every horizon step from an opaque zero
+  // and opaque leading dimensions: otherwise LICM hoists every (loop-invariant)
+  // per-lane LDS address of the unrolled layers out of the loop and spills them.
+#define PERSIST_LDS_LAYOUT(ZO, LDX, LDH, LDM, LDSS)                                         \
+  float* xin = smem + (ZO);                  /* ROWS x ldx  actor in / model in / next states */ \
+  float* h1 = xin + ROWS * (LDX);                                                             \
+  float* h2 = h1 + ROWS * (LDH);                                                              \
+  float* h3 = h2 + ROWS * (LDH);                                                              \
+  float* sraw = h3 + ROWS * (LDH);           /* ROWS x lds  states at the start of the step */  \
+  float* ao = sraw + ROWS * (LDSS);          /* ROWS x 20   actor head */                       \
+  float* dout = ao + ROWS * 20;                                                               \
+  float* lout = dout + ROWS * (LDM);                                                          \
+  float* act = lout + ROWS * (LDM);          /* ROWS x 8 */                                     \
+  float* rew = act + ROWS * 8;                                                                \
+  float* hval = rew + ROWS;                  /* ROWS x 8 */                                     \
+  float* nz_a = hval + ROWS * 8;             /* ROWS x 8    this step's action draws */         \
+  float* nz_m = nz_a + ROWS * 8;             /* ROWS x 64   this step's model draws */          \
+  int* flags = reinterpret_cast<int*>(nz_m + ROWS * 64);                                      \
+  int* alive = flags + ROWS;                                                                  \
+  int* s_nalive = alive + ROWS;                                                               \
+  float* red = reinterpret_cast<float*>(s_nalive + 4);  /* NW*RB*256 narrow partials */       \
+  float* vecs = red + NW * RB * 256;                    /* 4 x 64 */                          \
+  float* v_nm = vecs;                                                                         \
+  float* v_ns = vecs + 64;                                                                    \
+  float* v_lo = vecs + 128;                                                                   \
+  float* v_hi = vecs + 192;                                                                   \
+  (void)h3; (void)dout; (void)lout; (void)act; (void)rew; (void)hval; (void)nz_a; (void)nz_m;    \
+  (void)flags; (void)alive; (void)s_nalive; (void)red; (void)v_nm; (void)v_ns; (void)v_lo; (void)v_hi;
+  const int tile = blockIdx.x;
+  const int row0 = tile * ROWS;
+  const int nrows = min(ROWS, B - row0);
+  const int Ha = p.Ha, Hm = p.Hm;
+  const bool paired = S1 <= 16 && Hm == 200;
+  {
+  PERSIST_LDS_LAYOUT(0, p.ldx, p.ldh, p.ldm, p.lds)
+  if (tid < 256) {
+    const int j = tid & 63, w = tid >> 6;
+    if (w == 0 && j < S) v_nm[j] = p.norm_mean[j];
+    if (w == 1 && j < S) v_ns[j] = p.norm_std[j] + 1e-6f;
+    if (w == 2 && j < S1) v_lo[j] = p.min_lv[j];
+    if (w == 3 && j < S1) v_hi[j] = p.max_lv[j];
+  }
+
+  // ---- initial states (t = 0): chronological replay index -> physical row -----
+  const int kpad = round_up(S + A, 16);
+  for (int e = tid; e < ROWS * kpad; e += NT) {
+    const int r = e / kpad, k = e - r * kpad;
+    float v = 0.f;
+    if (r < nrows && k < S) {
+      const int64_t c = p.init_idx ? p.init_idx[row0 + r]
+                                   : prp_index((uint64_t)(row0 + r), (uint64_t)p.replay_len, p.prp_half_bits, p.prp_key);
+      const int64_t phys = (p.replay_ptr > p.replay_cap) ? (p.replay_ptr % p.replay_cap + c) % p.replay_cap : c;
+      v = p.replay_states[phys * S + k];
+    }
+    xin[r * p.ldx + k] = v;
+    if (k < S) sraw[r * p.lds + k] = v;
+  }
+  if (tid < ROWS) alive[tid] = tid < nrows;
+  persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, A, S1, B, 0, row0, nrows, nz_a, nz_m, 0, NT);   // step 0's draws
+  lds_barrier();
+  }
+  for (int t = 0; t < p.H; ++t) {
+    int zo = 0, ldx = p.ldx, ldh = p.ldh, ldm = p.ldm, ldss = p.lds;
+    asm volatile("" : "+s"(zo), "+s"(ldx), "+s"(ldh), "+s"(ldm), "+s"(ldss));
+    PERSIST_LDS_LAYOUT(zo, ldx, ldh, ldm, ldss)
+    const int m = p.members[t];
+    const float* aW2 = step_opaque(p.aW2);
+    const float* ab2 = step_opaque(p.ab2);
+    const float* mW1 = p.mW1 + (size_t)m * p.ms_in;
+    const float* mW2 = p.mW2 + (size_t)m * p.ms_hid;
+    const float* dW1 = p.dW1 + (size_t)m * p.ms_hid;
+    const float* dW2 = p.dW2 + (size_t)m * p.ms_out;
+    const float* lW1 = p.lW1 + (size_t)m * p.ms_hid;
+    const float* lW2 = p.lW2 + (size_t)m * p.ms_out;
+    const float* mb1 = p.mb1 + (size_t)m * Hm;
+    const float* mb2 = p.mb2 + (size_t)m * Hm;
+    const float* db1 = p.db1 + (size_t)m * Hm;
+    const float* db2 = p.db2 + (size_t)m * S1;
+    const float* lb1 = p.lb1 + (size_t)m * Hm;
+    const float* lb2 = p.lb2 + (size_t)m * S1;
+
+    if (t == 2) RSTAMP(0);
+    if (t == 2) RSTAMP(1);
+    // ---- actor MLP (src/policy.py:61-100) ------------------------------------
+    tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh);
+    lds_barrier();
+    if (t == 2) RSTAMP(2);
+    tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
+    lds_barrier();
+    if (t == 2) RSTAMP(3);
+    tile_dense_narrow<NW, RB, ACT_NONE>(h2, ldh, Ha, step_opaque(p.aW3), step_opaque(p.ab3), 2 * A, ao, 20, red);
+    lds_barrier();
+    if (t == 2) RSTAMP(4);
+
+    // ---- squashed Gaussian sample + model input [normalize(s), a] -------------
+    for (int e = tid; e < ROWS * A; e += NT) {
+      const int r = e / A, d = e - r * A;
+      const float mu = ao[r * 20 + d], raw = ao[r * 20 + A + d];
+      const float ls = -6.f + 10.f * sigmoidf(raw);
+      const float a = tanhf(nz_a[r * 8 + d] * expf(ls) + mu);
+      act[r * 8 + d] = a;
+      xin[r * ldx + S + d] = a;
+    }
+    for (int e = tid; e < ROWS * S; e += NT) {
+      const int r = e / S, k = e - r * S;
+      xin[r * ldx + k] = (sraw[r * ldss + k] - v_nm[k]) / v_ns[k];
+    }
+    lds_barrier();
+    if (t == 2) RSTAMP(5);
+
+    // ---- elite member forward (src/dynamics.py:112-122) -----------------------
+    tile_dense<NW, RB, MAXC, ACT_SILU>(xin, ldx, S + A, mW1, mb1, Hm, h1, ldh);
+    lds_barrier();
+    if (t == 2) RSTAMP(6);
+    tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, mW2, mb2, Hm, h2, ldh);
+    if (paired) {
+      lds_barrier();
+      if (t == 2) RSTAMP(7);
+      tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
+      lds_barrier();
+      if (t == 2) RSTAMP(8);
+      tile_dense_narrow_pair<NW, RB, ACT_NONE>(h1, h3, ldh, Hm, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm, red);
+    } else {
+      lds_barrier();
+      tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
+      lds_barrier();
+      if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm, red);
+      else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm);
+      lds_barrier();
+      tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, lW1, lb1, Hm, h1, ldh);
+      lds_barrier();
+      if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm, red);
+      else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm);
+    }
+    lds_barrier();
+    if (t == 2) RSTAMP(9);
+
+    // ---- residual mean, log-var soft clamp, Gaussian sample -------------------
+    for (int e = tid; e < ROWS * S1; e += NT) {
+      const int r = e / S1, j = e - r * S1;
+      const float mean = dout[r * ldm + j] + (j < S ? sraw[r * ldss + j] : 0.f);
+      float lv = lout[r * ldm + j];
+      lv = v_hi[j] - softplusf(v_hi[j] - lv);
+      lv = v_lo[j] + softplusf(lv - v_lo[j]);
+      const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
+      if (j < S) xin[r * ldx + j] = x;
+      else rew[r] = x;
+    }
+    lds_barrier();
+    if (t == 2) RSTAMP(10);
+
+    // ---- constraints, alive map of this step (wave 0); the other waves draw the
+    //      next step's noise meanwhile (this step's draws were consumed above) ----
+    if (t + 1 < p.H)
+      persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, A, S1, B, t + 1, row0, nrows, nz_a, nz_m, 64, NT - 64);
+    if (tid < 64) {
+      bool in_r = false, dn = false, vl = false;
+      if (tid < ROWS && alive[tid]) {
+        float hh[8];
+        env_constraints_row(p.env, xin + tid * ldx, dn, vl, hh);
+        for (int c = 0; c < C; ++c) hval[tid * 8 + c] = hh[c];
+        in_r = true;
+      }
+      if (tid < ROWS) flags[tid] = (dn ? 1 : 0) | (vl ? 2 : 0) | (in_r ? 4 : 0);   // bit2: row in this step
+      const uint64_t mk = __ballot(in_r);
+      if (in_r) p.inv[((size_t)t * p.ntiles + tile) * ROWS + __popcll(mk & ((1ull << tid) - 1ull))] = tid;
+      if (tid == 0) p.cnt[(size_t)t * p.ntiles + tile] = __popcll(mk);
+      const uint64_t still = __ballot(in_r && !dn);
+      if (tid < ROWS) alive[tid] = in_r && !dn;
+      if (tid == 0) *s_nalive = __popcll(still);
+    }
+    lds_barrier();
+    if (t == 2) RSTAMP(11);
+
+    // ---- staging writes (this step's surviving rows), next step's states -------
+    const size_t sb = (size_t)t * B + row0;
+    for (int e = tid; e < ROWS * S; e += NT) {
+      const int r = e / S, k = e - r * S;
+      const float x = xin[r * ldx + k];
+      if (flags[r] & 4) {
+        p.st_s[(sb + r) * S + k] = sraw[r * ldss + k];
+        p.st_s2[(sb + r) * S + k] = x;
+      }
+      sraw[r * ldss + k] = x;   // same element, same thread: no barrier needed
+    }
+    for (int e = tid; e < nrows * A; e += NT) {
+      const int r = e / A, d = e - r * A;
+      if (flags[r] & 4) p.st_a[(sb + r) * A + d] = act[r * 8 + d];
+    }
+    for (int e = tid; e < nrows * C; e += NT) {
+      const int r = e / C, c = e - r * C;
+      if (flags[r] & 4) p.st_h[(sb + r) * C + c] = hval[r * 8 + c];
+    }
+    if (tid < nrows && (flags[tid] & 4)) {
+      p.st_r[sb + tid] = rew[tid];
+      p.st_dv[sb + tid] = (uint8_t)(flags[tid] & 3);
+    }
+    if (t == 2) RSTAMP(12);
+    const int n_alive = __builtin_amdgcn_readfirstlane(*s_nalive);   // uniform exit
+    if (n_alive == 0) {   // the whole tile finished: later steps see no rows from it
+      for (int t2 = t + 1 + tid; t2 < p.H; t2 += NT) p.cnt[(size_t)t2 * p.ntiles + tile] = 0;
+      return;
+    }
+    lds_barrier();
+  }
+}
+
+#undef PERSIST_LDS_LAYOUT
+
+// per step t: exclusive prefix of the tile counts -> pos[t][tile], n[t]
+__global__ __launch_bounds__(256) void rollout_scan_kernel(const int* __restrict__ cnt, int* __restrict__ pos,
+                                                           int* __restrict__ n, int ntiles) {
+  __shared__ int part[256];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const int* c = cnt + (size_t)t * ntiles;
+  int* ps = pos + (size_t)t * ntiles;
+  const int per = (ntiles + 255) / 256, b0 = tid * per;
+  int run = 0;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < ntiles) run += c[b0 + i];
+  part[tid] = run;
+  __syncthreads();
+  if (tid < 64) {   // exclusive scan of the 256 partials in one wave
+    int v[4], sum = 0;
+    for (int q = 0; q < 4; ++q) { v[q] = part[tid * 4 + q]; sum += v[q]; }
+    int incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += y;
+    }
+    int e = incl - sum;
+    for (int q = 0; q < 4; ++q) { const int x = v[q]; part[tid * 4 + q] = e; e += x; }
+    if (tid == 63) n[t] = incl;
+  }
+  __syncthreads();
+  int e = part[tid];
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < ntiles) { ps[b0 + i] = e; e += c[b0 + i]; }
+}
+
+// staged rows -> circular virtual buffer, in the reference's order
+template <int ROWS>
+__global__ __launch_bounds__(256) void rollout_emit_kernel(PersistArgs p, const int* __restrict__ pos,
+                                                           const int* __restrict__ n, const int64_t* __restrict__ vptr,
+                                                           int64_t vcap, float* __restrict__ vs, float* __restrict__ va,
+                                                           float* __restrict__ vs2, float* __restrict__ vr,
+                                                           float* __restrict__ vh, uint8_t* __restrict__ vd,
+                                                           uint8_t* __restrict__ vv) {
+  __shared__ int64_t s_off;
+  const int t = blockIdx.y, tid = threadIdx.x;
+  if (tid == 0) {
+    int64_t o = 0;
+    for (int u = 0; u < t; ++u) o += n[u];
+    s_off = o + *vptr;
+  }
+  __syncthreads();
+  const int slot = blockIdx.x * 256 + tid;
+  const int tile = slot / ROWS, k = slot - tile * ROWS;
+  if (tile >= p.ntiles) return;
+  const size_t ti = (size_t)t * p.ntiles + tile;
+  if (k >= p.cnt[ti]) return;
+  const int S = p.S, A = p.A, C = p.C;
+  const size_t src = (size_t)t * p.B + (size_t)tile * ROWS + p.inv[ti * ROWS + k];
+  const int64_t q = (s_off + pos[ti] + k) % vcap;
+  for (int j = 0; j < S; ++j) {
+    vs[q * S + j] = p.st_s[src * S + j];
+    vs2[q * S + j] = p.st_s2[src * S + j];
+  }
+  for (int d = 0; d < A; ++d) va[q * A + d] = p.st_a[src * A + d];
+  for (int c = 0; c < C; ++c) vh[q * C + c] = p.st_h[src * C + c];
+  vr[q] = p.st_r[src];
+  const uint8_t dv = p.st_dv[src];
+  vd[q] = dv & 1;
+  vv[q] = (dv >> 1) & 1;
+}
+
+// off[t] = sum n[<t], off[H] = total; advance the buffer pointer
+__global__ void rollout_persist_finalize_kernel(int64_t* vptr, const int* n, int64_t* off, int H) {
+  int64_t o = 0;
+  for (int t = 0; t < H; ++t) {
+    off[t] = o;
+    o += n[t];
+  }
+  off[H] = o;
+  *vptr += o;
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 
@@ -400,13 +793,21 @@ struct RolloutWs {
 };
 
 // Byte offsets of the workspace pieces (in order); returns total bytes.
-static size_t rollout_ws_offsets(int B, int S, int H, size_t off[8]) {
-  const size_t bytes[8] = {sizeof(float) * (size_t)B * S, sizeof(float) * (size_t)B * S,
-                           sizeof(int) * ((size_t)B / 16 + 1), sizeof(int) * ((size_t)B / 16 + 1),
-                           sizeof(int) * (size_t)B, sizeof(int) * (size_t)B,
-                           sizeof(int) * (size_t)(H + 1), sizeof(int64_t) * (size_t)(H + 1)};
+// pieces 0-7: step-engine scratch + n/off; 8-16: fused-engine staging, indexed
+// [t][original row] (A, C <= 8 slots), per-(t, tile) counts / in-tile maps / positions
+constexpr int WS_PIECES = 17;
+static size_t rollout_ws_offsets(int B, int S, int H, size_t off[WS_PIECES]) {
+  const size_t HB = (size_t)H * B, T16 = (size_t)B / 16 + 1;
+  const size_t bytes[WS_PIECES] = {sizeof(float) * (size_t)B * S, sizeof(float) * (size_t)B * S,
+                                   sizeof(int) * T16, sizeof(int) * T16,
+                                   sizeof(int) * (size_t)B, sizeof(int) * (size_t)B,
+                                   sizeof(int) * (size_t)(H + 1), sizeof(int64_t) * (size_t)(H + 1),
+                                   sizeof(float) * HB * S, sizeof(float) * HB * S, sizeof(float) * HB * 8,
+                                   sizeof(float) * HB, sizeof(float) * HB * 8, HB,
+                                   sizeof(int) * (size_t)H * T16, sizeof(int) * (size_t)H * (B + 32),
+                                   sizeof(int) * (size_t)H * T16};
   size_t o = 0;
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < WS_PIECES; ++i) {
     off[i] = o;
     o += align256(bytes[i]);
   }
@@ -414,7 +815,7 @@ static size_t rollout_ws_offsets(int B, int S, int H, size_t off[8]) {
 }
 
 static RolloutWs rollout_ws(int B, int S, int H, char* base) {
-  size_t o[8];
+  size_t o[WS_PIECES];
   rollout_ws_offsets(B, S, H, o);
   RolloutWs w;
   w.nxt[0] = (float*)(base + o[0]);
@@ -429,14 +830,14 @@ static RolloutWs rollout_ws(int B, int S, int H, char* base) {
 }
 
 DRPO_API size_t drpo_rollout_workspace_size(int B, int S, int H) {
-  size_t o[8];
+  size_t o[WS_PIECES];
   return rollout_ws_offsets(B, S, H, o);
 }
 
 // Byte offset (inside the workspace) of the device int64 that holds the number of
 // transitions written by the last drpo_rollout call (off[H]).
 DRPO_API size_t drpo_rollout_count_offset(int B, int S, int H) {
-  size_t o[8];
+  size_t o[WS_PIECES];
   rollout_ws_offsets(B, S, H, o);
   return o[7] + sizeof(int64_t) * (size_t)H;
 }
@@ -445,6 +846,69 @@ static int hb_for(int64_t n) {
   int b = 1;
   while ((1ull << (2 * b)) < (uint64_t)n) ++b;
   return b;
+}
+
+// engine 2: fused-horizon kernel + count scan + ordered emit + pointer advance
+static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hipStream_t stream) {
+  DRPO_REQUIRE(d->H <= PERSIST_MAX_H, "drpo_rollout: engine 2 supports horizon <= %d", PERSIST_MAX_H);
+  const int S = d->S, A = d->A, S1 = d->S + 1, B = d->B, H = d->H;
+  size_t o[WS_PIECES];
+  rollout_ws_offsets(B, S, H, o);
+  char* base = (char*)d->workspace;
+  PersistArgs a{};
+  a.S = S; a.A = A; a.C = d->C; a.Ha = d->Ha; a.Hm = d->Hm; a.B = B; a.H = H;
+  a.ntiles = (B + rpt - 1) / rpt;
+  a.env.id = d->env_id; a.env.surr_start = d->tracking_surr_start; a.env.n_surr = d->tracking_n_surr;
+  a.env.quad_x_threshold = d->quad_x_threshold; a.env.quad_z_threshold = d->quad_z_threshold;
+  a.aW1 = d->aW1; a.ab1 = d->ab1; a.aW2 = d->aW2; a.ab2 = d->ab2; a.aW3 = d->aW3; a.ab3 = d->ab3;
+  a.mW1 = d->mW1; a.mb1 = d->mb1; a.mW2 = d->mW2; a.mb2 = d->mb2; a.dW1 = d->dW1; a.db1 = d->db1;
+  a.dW2 = d->dW2; a.db2 = d->db2; a.lW1 = d->lW1; a.lb1 = d->lb1; a.lW2 = d->lW2; a.lb2 = d->lb2;
+  a.ms_in = drpo_packed_size(S + A, d->Hm);
+  a.ms_hid = drpo_packed_size(d->Hm, d->Hm);
+  a.ms_out = drpo_packed_size(d->Hm, S1);
+  a.norm_mean = d->norm_mean; a.norm_std = d->norm_std; a.min_lv = d->min_lv; a.max_lv = d->max_lv;
+  a.replay_states = d->replay_states; a.init_idx = d->init_idx;
+  a.replay_len = rlen; a.replay_ptr = d->replay_ptr; a.replay_cap = d->replay_cap;
+  a.prp_half_bits = hb_for(rlen);
+  for (int i = 0; i < 4; ++i) a.prp_key[i] = (uint32_t)(d->seed >> (8 * i)) * 0x9E3779B9u + (uint32_t)d->ctr * (2 * i + 1) + i;
+  a.eps_a = d->eps_a; a.eps_m = d->eps_m;
+  a.seed = d->seed; a.ctr = d->ctr;
+  a.st_s = (float*)(base + o[8]); a.st_s2 = (float*)(base + o[9]); a.st_a = (float*)(base + o[10]);
+  a.st_r = (float*)(base + o[11]); a.st_h = (float*)(base + o[12]); a.st_dv = (uint8_t*)(base + o[13]);
+  a.cnt = (int*)(base + o[14]); a.inv = (int*)(base + o[15]);
+  int* pos = (int*)(base + o[16]);
+  int* n = (int*)(base + o[6]);
+  int64_t* off = (int64_t*)(base + o[7]);
+  a.ldx = lds_ld(S + A);
+  a.ldh = lds_ld(d->Ha > d->Hm ? d->Ha : d->Hm);
+  a.ldm = round_up(S1, 16) + 4;
+  a.lds = round_up(S, 4);
+  for (int t = 0; t < H; ++t) a.members[t] = d->members[t];
+
+  constexpr int NW = 8;
+  const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 3 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 8 +
+                                                           64 + 2) + 4 + (size_t)NW * (rpt / 16) * 256 + 256);
+  DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
+  if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
+  if (rpt == 32)
+    rollout_persist_kernel<2, NW><<<a.ntiles, NW * 64, lds_bytes, stream>>>(a);
+  else
+    rollout_persist_kernel<1, NW><<<a.ntiles, NW * 64, lds_bytes, stream>>>(a);
+  DRPO_LAUNCH_CHECK("rollout_persist");
+  if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[1], stream);
+  rollout_scan_kernel<<<H, 256, 0, stream>>>(a.cnt, pos, n, a.ntiles);
+  DRPO_LAUNCH_CHECK("rollout_scan");
+  const dim3 eg((unsigned)((a.ntiles * rpt + 255) / 256), (unsigned)H);
+  if (rpt == 32)
+    rollout_emit_kernel<32><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, d->vcap, d->vs, d->va, d->vs2, d->vr, d->vh,
+                                                    d->vd, d->vv);
+  else
+    rollout_emit_kernel<16><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, d->vcap, d->vs, d->va, d->vs2, d->vr, d->vh,
+                                                    d->vd, d->vv);
+  DRPO_LAUNCH_CHECK("rollout_emit");
+  rollout_persist_finalize_kernel<<<1, 1, 0, stream>>>(d->vptr, n, off, H);
+  DRPO_LAUNCH_CHECK("rollout_finalize");
+  return DRPO_OK;
 }
 
 DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
@@ -469,6 +933,15 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
   const int rpt = d->rows_per_tile ? d->rows_per_tile : (d->B >= 256 * 32 ? 32 : 16);
   DRPO_REQUIRE(rpt == 16 || rpt == 32, "drpo_rollout: rows_per_tile must be 16 or 32");
   const int S = d->S, A = d->A, S1 = d->S + 1;
+  DRPO_REQUIRE(d->engine >= 0 && d->engine <= 2 && (d->eps_layout == 0 || d->eps_layout == 1),
+               "drpo_rollout: engine %d / eps_layout %d", d->engine, d->eps_layout);
+  DRPO_REQUIRE((d->eps_a == nullptr) == (d->eps_m == nullptr), "drpo_rollout: eps_a and eps_m go together");
+  int engine = d->engine;
+  if (engine == 0) engine = (d->eps_a && d->eps_layout == 0) || d->H > PERSIST_MAX_H ? 1 : 2;
+  if (d->eps_a)
+    DRPO_REQUIRE(d->eps_layout == engine - 1, "drpo_rollout: eps_layout %d cannot drive engine %d (compacted draws "
+                 "need engine 1, original-row draws engine 2)", d->eps_layout, engine);
+  if (engine == 2) return rollout_fused(d, rpt, rlen, stream);
 
   RolloutStepArgs a{};
   a.S = S; a.A = A; a.C = d->C; a.Ha = d->Ha; a.Hm = d->Hm; a.Bmax = d->B;

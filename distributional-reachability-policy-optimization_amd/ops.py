@@ -63,7 +63,14 @@ class EventTimer:
         return out
 
 
-def rollout(alg, policy, initial_states, noise, timer=None):
+def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
+    """One imagined rollout (src/smbpo.py:229-249) into alg.virt_buffer.
+
+    Engine (``alg.rollout_engine``, 0 = auto): 2 = fused horizon kernel (default for
+    device noise), 1 = one launch per horizon step (used for recorded reference
+    draws, which are indexed by the compacted row of each step). ``eps_layout=1``
+    marks a tape whose per-step draws are indexed by the original batch row
+    ([B] rows every step), which drives engine 2 with recorded draws."""
     L = _lib.lib()
     dev = alg.device
     B, H = alg.rollout_batch_size, alg.horizon
@@ -133,7 +140,13 @@ def rollout(alg, policy, initial_states, noise, timer=None):
     d.vptr, d.vcap = vb._pointer.data_ptr(), vb.capacity
     d.workspace = ws.data_ptr()
     d.rows_per_tile = getattr(alg, 'rows_per_tile', 0)
+    engine = getattr(alg, 'rollout_engine', 0)
+    if engine == 0:
+        engine = 1 if (noise.parity and eps_layout == 0) or H > 128 else 2
+    d.engine, d.eps_layout = engine, (eps_layout if noise.parity else 0)
     d.step_events = timer.events if timer is not None else None
+    if timer is not None:
+        timer.pairs = 1 if engine == 2 else H   # engine 2: one pair around the fused kernel
     _lib.check(L.drpo_rollout(ctypes.byref(d), _lib.stream()), 'rollout')
     vb._device_advanced()
     off = L.drpo_rollout_count_offset(B, S, H)

@@ -52,8 +52,11 @@ int drpo_event_elapsed_ms(float* ms /* host */, void* start, void* stop);
  * SquashedGaussianPolicy.act(eval=False) (src/policy.py:77-97), the env
  * check_done / check_violation / get_constraint_values round trips
  * (src/smbpo.py:63-65) and ConstraintSafetySampleBuffer.extend into the virtual
- * buffer (src/sampling.py:128-145): one fused kernel per horizon step, rows that
- * are done are compacted away (order preserving) on the device.            */
+ * buffer (src/sampling.py:128-145). Rows that are done leave the batch; the
+ * buffer receives each step's surviving rows in order, as the reference's
+ * next_states[~dones] compaction does. Engine 1 runs one kernel per horizon
+ * step; engine 2 (default) keeps each row tile on one workgroup for the whole
+ * horizon and orders the rows into the buffer afterwards.                   */
 typedef struct {
   int S, A, C, Ha, Hm, B, H;
   int env_id, tracking_surr_start, tracking_n_surr;
@@ -74,7 +77,11 @@ typedef struct {
   int64_t vcap;
   void* workspace;               /* drpo_rollout_workspace_size bytes */
   int rows_per_tile;             /* 16 or 32, 0 = auto */
-  void** step_events;            /* optional [2*H] events recorded around each step kernel */
+  void** step_events;            /* optional [2*H] events: engine 1 records pair t around step t's kernel,
+                                    engine 2 records pair 0 around the fused horizon kernel */
+  int engine;                    /* 0 auto, 1 one launch per horizon step, 2 fused horizon (persistent per tile) */
+  int eps_layout;                /* eps_a/eps_m rows: 0 compacted per step (reference draw order; engine 1),
+                                    1 original batch row (row i of step t = trajectory i; engine 2) */
 } drpo_rollout_desc_t;
 
 size_t drpo_rollout_workspace_size(int B, int S, int H);

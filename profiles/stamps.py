@@ -69,7 +69,8 @@ def rollout_stamps():
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)
-    alg.horizon = 1
+    alg.horizon = int(os.environ.get('DRPO_STAMPS_H', '1'))   # stamps keep the last step's launch
+    alg.rollout_engine = 1
     for _ in range(3):
         alg.rollout(alg.actor)
     torch.cuda.synchronize()
@@ -87,5 +88,37 @@ def rollout_stamps():
     print(f'   total {tot:.0f} cycles')
 
 
-if __name__ == '__main__' and os.environ.get('DRPO_STAMPS_ROLLOUT'):
+def fused_stamps():
+    """Phase timing of rollout_persist_kernel (horizon step t=2 of a bench rollout)."""
+    import bench
+    from drpo_amd import _lib
+    L = _lib.lib()
+    L.drpo_debug_stamps_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device('cuda')
+    alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON)
+    rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
+    alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
+    alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
+    bench.steady_mode(alg)
+    alg.rollout_engine = 2
+    for _ in range(3):
+        alg.rollout(alg.actor)
+    torch.cuda.synchronize()
+    buf = np.zeros((1 << 14, 16), np.uint64)
+    L.drpo_debug_stamps_rollout(buf.ctypes.data, 256)
+    st = buf[:256].astype(np.int64)
+    names = ['start', 'noise', 'actor L1', 'actor L2', 'actor L3', 'sample', 'member L1', 'member L2', 'pair L1',
+             'pair L2', 'gauss', 'constraints', 'staging']
+    print('== rollout_persist_kernel step t=2 (B=4096, quadrotor): cycles per phase, mean over 256 workgroups')
+    tot = 0
+    for c in range(1, 13):
+        d = st[:, c] - st[:, c - 1]
+        tot += d.mean()
+        print(f'   {names[c]:12s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f}')
+    print(f'   total {tot:.0f} cycles')
+
+
+if __name__ == '__main__' and os.environ.get('DRPO_STAMPS_ROLLOUT') == 'fused':
+    fused_stamps()
+elif __name__ == '__main__' and os.environ.get('DRPO_STAMPS_ROLLOUT'):
     rollout_stamps()

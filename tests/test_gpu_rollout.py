@@ -36,11 +36,9 @@ def test_rollout_matches_reference_fixture(env):
         close(got[k], d['out/' + k], msg=k)
 
 
-@pytest.mark.parametrize('env,B,H', [('quadrotor', 4096, 10), ('point-robot', 1024, 20), ('tracking', 512, 8),
-                                     ('cartpole', 256, 5)])
-def test_rollout_matches_oracle_full_width(env, B, H):
-    """Default widths (actor 256, model 200, E=7) at BASELINE-like shapes vs the oracle
-    driven by the live reference RNG calls; the recorded draws are fed to the HIP path."""
+def _full_width_case(env, B, H):
+    """SMBPO at default widths + a replay of N states, and the oracle's rollout
+    driven by live reference RNG calls (returns alg, oracle output, recorded draws)."""
     torch.manual_seed(5)
     cfg = drpo_amd.SMBPO.Config()
     cfg.update({'horizon': H, 'rollout_batch_size': B, 'buffer_max': max(B * H, 20000)})
@@ -71,13 +69,100 @@ def test_rollout_matches_oracle_full_width(env, B, H):
     P.update({k: v for k, v in sd.items() if k.startswith('model_ensemble.')})
     live = O.LiveRNG()
     ref = O.rollout(P, 'actor.net.', 'model_ensemble.', m._elite_inds, st, env, B, H, live)
-    out = alg.rollout(alg.actor, noise=drpo_amd.TapeNoise(live.entries))
+    return alg, ref, live.entries
+
+
+FULL_WIDTH = [('quadrotor', 4096, 10), ('point-robot', 1024, 20), ('tracking', 512, 8), ('cartpole', 256, 5)]
+
+
+@pytest.mark.parametrize('env,B,H', FULL_WIDTH)
+def test_rollout_matches_oracle_full_width(env, B, H):
+    """Default widths (actor 256, model 200, E=7) at BASELINE-like shapes vs the oracle
+    driven by the live reference RNG calls; the recorded draws are fed to the HIP path
+    (compacted per-step draws -> the per-step engine)."""
+    alg, ref, entries = _full_width_case(env, B, H)
+    out = alg.rollout(alg.actor, noise=drpo_amd.TapeNoise(entries))
     torch.cuda.synchronize()
     n = len(ref['states'])
     assert len(out) == n
     got = out.get(as_dict=True)
     for k in COMP:
         close(got[k], ref[k], tol=2e-4, msg=k)
+
+
+def original_row_tape(entries, ref, B):
+    """Re-index the reference's per-step draws (row k of step t = k-th surviving row)
+    by original batch row: step t's arrays become [B, dim], row i = trajectory i
+    (zeros for rows already done). Survivors follow from the oracle's dones:
+    step t+1 keeps step t's rows with done == 0, in order (src/smbpo.py:243-246)."""
+    ids = np.arange(B)
+    out, off, t_rows = [], 0, None
+    dones = np.asarray(ref['dones']).astype(bool)
+    for kind, v in entries:
+        if kind == 'normal':               # eps_a of a step: [n_t, A]
+            n = v.shape[0]
+            assert n == len(ids)
+            full = np.zeros((B, v.shape[1]), np.float32)
+            full[ids] = v
+            out.append((kind, full))
+            t_rows = n
+        elif kind == 'randn_like':         # eps_m of the same step: [n_t, S+1]
+            full = np.zeros((B, v.shape[1]), np.float32)
+            full[ids] = v
+            out.append((kind, full))
+            ids = ids[~dones[off:off + t_rows]]
+            off += t_rows
+        else:
+            out.append((kind, v))
+    assert off == len(dones)
+    return out
+
+
+@pytest.mark.parametrize('env,B,H', FULL_WIDTH)
+def test_fused_engine_matches_oracle_full_width(env, B, H):
+    """The fused-horizon engine (production default) against the same oracle run,
+    its recorded draws re-indexed by original row (rows die in these cases, so the
+    tile masking, per-(step, tile) counts and the ordered emit are all exercised)."""
+    alg, ref, entries = _full_width_case(env, B, H)
+    tape = drpo_amd.TapeNoise(original_row_tape(entries, ref, B))
+    from drpo_amd import ops
+    out = ops.rollout(alg, alg.actor, None, tape, eps_layout=1)
+    torch.cuda.synchronize()
+    assert tape.done()
+    n = len(ref['states'])
+    assert len(out) == n
+    assert len(alg.virt_buffer) == n
+    got = out.get(as_dict=True)
+    for k in COMP:
+        close(got[k], ref[k], tol=2e-4, msg=k)
+
+
+@pytest.mark.parametrize('B,H,rpt', [(4096, 10, 0), (1000, 7, 0), (8192, 4, 32), (8192, 3, 16)])
+def test_fused_engine_matches_step_engine_device_noise(B, H, rpt):
+    """Production noise (Philox keyed by row and step): with no row finishing the two
+    engines draw identical numbers, so their buffers must agree to rounding (bench
+    workload in steady mode, plus ragged and 32-row-tile shapes)."""
+    import random
+    import bench
+    outs = []
+    for engine in (1, 2):
+        random.seed(11)
+        alg = bench.make_alg(DEV, B, H, 7, 0, bench.QUAD_JSON)
+        rep = bench.synth_replay(12, 2, 2, 20000, np.random.RandomState(0))
+        alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(DEV) for k, v in rep.items()})
+        alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
+        bench.steady_mode(alg)
+        alg.rollout_engine, alg.rows_per_tile = engine, rpt
+        out = alg.rollout(alg.actor, noise=drpo_amd.DeviceNoise(1234))
+        torch.cuda.synchronize()
+        assert len(out) == B * H
+        outs.append(out.get(as_dict=True))
+    for k in COMP:
+        a, b = outs[0][k], outs[1][k]
+        if a.dtype == torch.bool:
+            assert torch.equal(a, b), k
+        else:
+            close(a, b, tol=1e-5, msg=k)
 
 
 def test_rollout_production_mode_runs_and_conserves_rows():
