@@ -52,6 +52,13 @@ def sac_flop_per_step(B, S=12, A=2, C=2, H=256):
     return 2 * B * (critic + actor / 2 + mult / 5)
 
 
+def fit_flop_per_step(S, A, E, b, Hm=200):
+    """one fit step = forward + backward (2x) over E*b rows of the
+    member MLP (trunk + both heads): 3 x 2 x MACs."""
+    mac = (S + A) * Hm + Hm * Hm + 2 * (Hm * Hm + Hm * (S + 1))
+    return 3 * 2 * mac * E * b
+
+
 def synth_replay(S, A, C, N, rng):
     s = rng.normal(0, 0.1, size=(N, S)).astype(np.float32)
     s[:, 0] = rng.uniform(-1, 1, N)
@@ -161,6 +168,9 @@ def main():
     ap.add_argument('--rollout-only', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--no-fit', action='store_true', help='skip the model-fit post-pass')
+    ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N>1 (nccl = RCCL)')
+    ap.add_argument('--fit-steps', type=int, default=50)
     ap.add_argument('--engine', type=int, default=0, help='rollout engine: 0 auto (fused horizon), 1 per-step launches')
     args = ap.parse_args()
 
@@ -168,10 +178,15 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
+    # --backend gloo + more ranks than GPUs: a rehearsal of the N>1 path on one box
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     B, H, E = args.batch, args.horizon, args.ensemble
@@ -244,9 +259,10 @@ def main():
         wall, roll_s, sac_s, n_all = tot[0].item(), tot[1].item(), tot[2].item(), tot[3].item()
 
     # post-pass (untimed): per-kernel-class MLP throughput of the SAC update from HIP
-    # events around every MLP launch (drpo_amd.sac_step.LaunchProfiler)
+    # events around every MLP launch (drpo_amd.sac_step.LaunchProfiler). Every rank
+    # runs it (the updates all-reduce gradients); rank 0 reports.
     sac_kernels = None
-    if do_sac and rank == 0:
+    if do_sac:
         from drpo_amd.sac_step import LaunchProfiler
         eng = alg.solver.engine
         eng.profiler = LaunchProfiler()
@@ -258,6 +274,36 @@ def main():
         sac_kernels = {k: {'tflops': round(v['tflops'], 2), 'frac': round(v['tflops'] / FP32_PEAK_TFLOPS, 4),
                            'avg_launch_us': round(v['avg_ms'] * 1e3, 2), 'launches': v['launches']}
                        for k, v in summ.items() if ':' not in k}
+
+    # model fit ("report the model-fit step time separately"): one
+    # fit(steps=K) of the reference's E x 256-row steps on the synthetic replay; under
+    # torchrun the members are sharded over the ranks (distributed.MemberShard)
+    fit_res = None
+    if not args.no_fit:
+        m = alg.model_ensemble
+        m.fit(alg.replay_buffer, steps=2)            # warm-up (workspaces, packing)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        f0 = time.perf_counter()
+        m.fit(alg.replay_buffer, steps=args.fit_steps)   # ends with a host read of the losses
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        fit_s = torch.tensor([time.perf_counter() - f0], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(fit_s, op=dist.ReduceOp.MAX)
+        fit_s = fit_s.item()
+        from drpo_amd.distributed import member_sharding
+        sh = member_sharding(m)
+        fl = fit_flop_per_step(12, 2, E, m.batch_size, m.hidden_dim)
+        fit_res = {'steps': args.fit_steps, 'ms_per_fit_step': fit_s / args.fit_steps * 1e3,
+                   'fit_steps_per_s': args.fit_steps / fit_s, 'flop_per_fit_step': fl,
+                   'achieved_tflops_job': fl * args.fit_steps / fit_s / 1e12,
+                   'rows_per_step': E * m.batch_size,
+                   'sharding': f'members {sh.ranges}' if sh is not None else
+                   ('batch (gradient all-reduce)' if world > 1 else 'single')}
+        steady_mode(alg)
 
     if rank != 0:
         if dist is not None:
@@ -290,6 +336,7 @@ def main():
                 'achieved_tflops_per_gpu': (sac_flop_per_step(B) * alg.solver_updates_per_step * args.steps / sac_s / 1e12)
                 if do_sac and sac_s > 0 else None,
                 'mlp_kernels': sac_kernels},
+        'model_fit': fit_res,
         'roofline': {'kernel': kname, 'bound': 'mfma', 'achieved': achieved,
                      'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_PEAK_TFLOPS,
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,

@@ -80,3 +80,87 @@ def sync_parameters(alg, src=0):
     for g in (sol.actor.group, sol.actor_safe.group, sol.critic_group, sol.critic_target_group, sol.multiplier.group,
               m.group):
         g.mark_dirty()
+
+
+class MemberShard:
+    """Ensemble-sharded model fit (SURVEY.md §8(e) "model fit"): rank r trains the
+    members [z0, z1) of the E-member ensemble. Members are independent except for
+
+      * the shared soft log-var bounds (min/max_log_var, 2(S+1) floats): their
+        gradients are sum-all-reduced every step (the bound term's own gradient
+        is added by rank 0 only);
+      * the holdout MSEs: every rank scores its own members on the SAME holdout
+        rows (broadcast from rank 0), then one sum-all-reduce of an [E] vector
+        gives every rank the identical argsort -> identical elites;
+      * after the fit every rank needs every member for rollouts: one all-gather
+        per [E, out, in] layer tensor (members are the leading dimension, so a
+        shard is one contiguous slice), broadcasts from each owner when E does
+        not divide evenly.
+
+    Per step this exchanges 2(S+1) floats instead of the whole ensemble gradient
+    (quadrotor E=32: 19.5 MB), and the per-step algorithm is exactly the
+    reference's (each member sees its own 256 rows of the E*256 draw)."""
+
+    def __init__(self, E, world=None, rank_=None, group=None):
+        self.E = E
+        self.world = world_size() if world is None else world
+        self.rank = rank() if rank_ is None else rank_
+        self.group = group
+        base, rem = divmod(E, self.world)
+        self.ranges = []
+        z = 0
+        for r in range(self.world):
+            c = base + (1 if r < rem else 0)
+            self.ranges.append((z, z + c))
+            z += c
+        self.z0, self.z1 = self.ranges[self.rank]
+
+    @property
+    def count(self):
+        return self.z1 - self.z0
+
+    @property
+    def even(self):
+        return self.E % self.world == 0
+
+    def sum_(self, t):
+        if self.world > 1:
+            _dist.all_reduce(t, group=self.group)
+
+    def broadcast_(self, *ts, src=0):
+        if self.world > 1:
+            for t in ts:
+                _dist.broadcast(t, src, group=self.group)
+
+    def merge_members(self, part, full):
+        """part [count, ...] (this rank's members) -> full [E, ...] on every rank."""
+        full[self.z0:self.z1].copy_(part)
+        self.gather_members_(full)
+        return full
+
+    def gather_members_(self, t):
+        """t [E, ...]: every rank's own slice -> replicated on all ranks (in place)."""
+        if self.world == 1:
+            return t
+        if self.even and _dist.get_backend(self.group) == 'nccl':
+            own = t[self.z0:self.z1].clone()
+            _dist.all_gather_into_tensor(t, own, group=self.group)
+        else:
+            for r, (a, b) in enumerate(self.ranges):
+                if b > a:
+                    _dist.broadcast(t[a:b], r, group=self.group)
+        return t
+
+
+def member_sharding(model):
+    """The ensemble's fit mode: a MemberShard when the job is data-parallel over
+    >1 ranks and the ensemble has at least one member per rank (config
+    ``dp_mode`` 'auto' | 'members'), else None (batch data parallelism)."""
+    mode = getattr(model, 'dp_mode', 'auto')
+    if not is_active() or mode == 'batch':
+        return None
+    if world_size() > model.ensemble_size:
+        if mode == 'members':
+            raise ValueError(f'dp_mode=members needs ensemble_size >= world size ({world_size()})')
+        return None
+    return MemberShard(model.ensemble_size)

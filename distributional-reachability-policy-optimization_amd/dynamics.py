@@ -47,6 +47,9 @@ class BatchedGaussianEnsemble(Configurable, Module):
         batch_size = 256
         learning_rate = 1e-3
         holdout_size = 256
+        # multi-GPU fit: 'auto' shards members over ranks when E >= world size
+        # (distributed.MemberShard), 'batch' all-reduces whole-ensemble gradients
+        dp_mode = 'auto'
 
     def __init__(self, config, state_dim, action_dim, device=default_device, optimizer_factory=None):
         Configurable.__init__(self, config)

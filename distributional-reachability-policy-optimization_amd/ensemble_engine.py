@@ -57,7 +57,9 @@ class EnsembleEngine:
         m = self.m
         return (('trunk.', m.trunk_spec), ('diff_head.', m.diff_spec), ('log_var_head.', m.logvar_spec))
 
-    def _nets(self, member=None, grads=False):
+    def _nets(self, member=None, grads=False, z0=0):
+        """Kernel views of the trunk and both heads: one member (``member``) or the
+        members from ``z0`` on (member stride; z0 > 0 for an ensemble shard)."""
         g = self.m.group
         nets, strides = [], []
         for prefix, spec in self._specs():
@@ -72,23 +74,24 @@ class EnsembleEngine:
                     st.append((0, 0))
                 else:          # packed-mirror stride per member, bias stride
                     st.append((W.shape[1], dout))
-                    W, WT = W[0], WT[0]
+                    W, WT, b = W[z0], WT[z0], b[z0]
                 lay.append((W, b, din, dout, ACT_ID[act], WT))
                 if grads:
-                    gl.append((g.view(f'{prefix}{2 * i}.weight', g.grad), g.view(f'{prefix}{2 * i}.bias', g.grad)))
+                    gl.append((g.view(f'{prefix}{2 * i}.weight', g.grad)[z0],
+                               g.view(f'{prefix}{2 * i}.bias', g.grad)[z0]))
             nets.append(Net(lay, gl if grads else None))
             strides.append(st)
         return nets, strides
 
     # ------------------------------------------------------------------ forward
-    def _forward(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False):
+    def _forward(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False, z0=0):
         """Raw head outputs (D, LVR) [Z*n, S+1]; with save=True the activations needed
         for the backward pass are kept (returns nets too)."""
         m, L = self.m, _lib.lib()
         S, A = m.state_dim, m.action_dim
         S1 = S + 1
         m.group.ensure_packed()
-        nets, strides = self._nets(member, grads=save)
+        nets, strides = self._nets(member, grads=save, z0=z0)
         rows = Z * n
         if save:
             for j, net in enumerate(nets):
@@ -180,7 +183,7 @@ class EnsembleEngine:
         return o['s2'], o['r']
 
     # ------------------------------------------------------------------ loss / grads
-    def _loss(self, nets, s, s_zs, t, t_zs, b, Z, grads, gscale=None, loss_out=None, tag='f'):
+    def _loss(self, nets, s, s_zs, t, t_zs, b, Z, grads, gscale=None, loss_out=None, tag='f', bound=True):
         m, L = self.m, _lib.lib()
         S = m.state_dim
         S1 = S + 1
@@ -192,7 +195,8 @@ class EnsembleEngine:
             gD, gL = self.buf(f'{tag}.gD', Z * b, S1), self.buf(f'{tag}.gL', Z * b, S1)
             gmin, gmax = g.view('min_log_var', g.grad), g.view('max_log_var', g.grad)
         _lib.check(L.drpo_ens_loss(_lib.ptr(D), _lib.ptr(LVR), _lib.ptr(s), s_zs, _lib.ptr(t), t_zs, b, S, Z,
-                                   _lib.ptr(m.min_log_var), _lib.ptr(m.max_log_var), float(m.log_var_bound_weight),
+                                   _lib.ptr(m.min_log_var), _lib.ptr(m.max_log_var),
+                                   float(m.log_var_bound_weight) if bound else 0.0,
                                    _lib.ptr(gscale), _lib.ptr(mse), _lib.ptr(loss_out), _lib.ptr(gD), _lib.ptr(gL),
                                    _lib.ptr(gmin), _lib.ptr(gmax), _lib.stream()), 'ens_loss')
         return mse, gD, gL
@@ -235,6 +239,10 @@ class EnsembleEngine:
 
     # ------------------------------------------------------------------ fit
     def fit(self, buffer, steps, noise=None):
+        """fit(steps=) (src/dynamics.py:155-183). Under data parallelism the members are
+        sharded over the ranks (distributed.MemberShard) unless dp_mode='batch', in which
+        case every rank fits all members on its own draw and the gradients are averaged."""
+        from .distributed import member_sharding
         m, L = self.m, _lib.lib()
         nz = self._noise(noise)
         rb = getattr(buffer, '_module', buffer)
@@ -242,18 +250,25 @@ class EnsembleEngine:
         n = len(rb)
         S, A = m.state_dim, m.action_dim
         S1 = S + 1
+        sh = member_sharding(m)
         # Normalizer over the chronological states (physical rows [0, n) hold the same set)
         m.state_normalizer.fit(rb._states[:n])
+        if sh is not None:       # one normalizer for the whole ensemble (rank 0's replay)
+            sh.broadcast_(m.state_normalizer.mean, m.state_normalizer.std)
         E, b = m.ensemble_size, m.batch_size
-        rows = E * b
+        z0, Z = (sh.z0, sh.count) if sh is not None else (0, E)
+        rows = Z * b
         xs, xa, xt = self.buf('fit.s', rows, S), self.buf('fit.a', rows, A), self.buf('fit.t', rows, S1)
         losses = torch.empty(max(steps, 1), device=self.dev)
         ptr_dev = rb._pointer if rb._host_ptr is None else None
         ptr_host = rb._host_ptr if rb._host_ptr is not None else 0
 
-        def gather(count, out):
-            idx = nz.randint(n, count) if nz.parity else None
-            idx_t = None if idx is None else torch.from_numpy(idx).to(self.dev)
+        def gather(count, out, full=None):
+            # parity mode: the reference's randint over all E*b rows, this shard's slice
+            idx = nz.randint(n, full or count) if nz.parity else None
+            if idx is not None and full:
+                idx = idx[z0 * b:z0 * b + count]
+            idx_t = None if idx is None else torch.from_numpy(np.ascontiguousarray(idx)).to(self.dev)
             ctr = 0 if nz.parity else nz.next()
             _lib.check(L.drpo_ens_gather(_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states),
                                          _lib.ptr(rb._rewards), ptr_host, _lib.ptr(ptr_dev), rb.capacity, count,
@@ -262,28 +277,68 @@ class EnsembleEngine:
 
         g = m.group
         g.grad.zero_()
+        if sh is None:
+            segs = lambda sc: [m.optimizer.segment(0, g.size, sc, zero_grad=True, pack_map=g.pack_map())]  # noqa
+        else:
+            ranges = self._shard_ranges(z0, Z)
+            lo, hi = g.offset('min_log_var'), g.offset('max_log_var') + S1
+            bounds_grad = g.grad[lo:hi]
+            pmap = g.pack_map()
+            segs = lambda sc: [m.optimizer.segment(a, c, sc, zero_grad=True, pack_map=pmap) for a, c in ranges]  # noqa
         for i in range(steps):
-            gather(rows, (xs, xa, xt))
-            nets, strides, save_x = self._forward(xs, xa, b, E, b * S, b * A, tag='fit', save=True)
-            _, gD, gL = self._loss(nets, xs, b * S, xt, b * S1, b, E, True, loss_out=losses[i], tag='fit')
-            self._backward(nets, strides, save_x, gD, gL, b, E)
-            self.dp.mean_(g.grad)
+            gather(rows, (xs, xa, xt), full=E * b if sh is not None else None)
+            nets, strides, save_x = self._forward(xs, xa, b, Z, b * S, b * A, tag='fit', save=True, z0=z0)
+            _, gD, gL = self._loss(nets, xs, b * S, xt, b * S1, b, Z, True, loss_out=losses[i], tag='fit',
+                                   bound=sh is None or sh.rank == 0)
+            self._backward(nets, strides, save_x, gD, gL, b, Z)
+            if sh is None:
+                self.dp.mean_(g.grad)
+            else:
+                sh.sum_(bounds_grad)      # shared log-var bounds: the sum over all members
             # Adam + grad zeroing + packed-mirror refresh in one launch
-            fused_step([m.optimizer.segment(0, g.size, m.optimizer.step_scalars(), zero_grad=True,
-                                            pack_map=g.pack_map())])
+            fused_step(segs(m.optimizer.step_scalars()))
         # holdout: the same rows for every member (src/dynamics.py:175-183)
         hb = m.holdout_size
         assert hb == b, 'reference asserts holdout_size == batch_size (src/dynamics.py:177)'
         hs, ha, ht = self.buf('ho.s', hb, S), self.buf('ho.a', hb, A), self.buf('ho.t', hb, S1)
         gather(hb, (hs, ha, ht))
-        nets, _, _ = self._forward(hs, ha, hb, E, 0, 0, tag='ho')
-        mse, _, _ = self._loss(nets, hs, 0, ht, 0, hb, E, False, tag='ho')
-        self.dp.mean_(mse)       # identical elites on every rank
+        if sh is not None:
+            sh.broadcast_(hs, ha, ht)
+        nets, _, _ = self._forward(hs, ha, hb, Z, 0, 0, tag='ho', z0=z0)
+        mse, _, _ = self._loss(nets, hs, 0, ht, 0, hb, Z, False, tag='ho')
+        if sh is None:
+            self.dp.mean_(mse)       # identical elites on every rank
+        else:
+            mse = sh.merge_members(mse, torch.zeros(E, device=self.dev))
+            sh.sum_(losses)          # per-step loss = sum of the shards' member terms
+            self._gather_members(sh)
         mse_h = mse.tolist()
         m.holdout_losses = mse_h
         m._elite_inds = [int(i) for i in np.argsort(np.asarray(mse_h, np.float32), kind='stable')[:m.num_elites]]
         return [float(x) for x in losses[:steps].tolist()]
 
+    def _shard_ranges(self, z0, Z):
+        """Flat-group element ranges of members [z0, z0+Z) of every layer, plus the
+        shared log-var bounds (the Adam segments of a member shard)."""
+        g, out = self.m.group, []
+        for prefix, spec in self._specs():
+            for i in range(spec.n_layers):
+                for key in (f'{prefix}{2 * i}.weight', f'{prefix}{2 * i}.bias'):
+                    off, shape = g.entries[key]
+                    per = int(np.prod(shape[1:]))
+                    out.append((off + z0 * per, off + (z0 + Z) * per))
+        S1 = self.m.state_dim + 1
+        out.append((g.offset('min_log_var'), g.offset('max_log_var') + S1))
+        return out
+
+    def _gather_members(self, sh):
+        """Every member's weights on every rank after a sharded fit."""
+        g = self.m.group
+        for prefix, spec in self._specs():
+            for i in range(spec.n_layers):
+                for key in (f'{prefix}{2 * i}.weight', f'{prefix}{2 * i}.bias'):
+                    sh.gather_members_(g.view(key))
+        g.mark_dirty()
 
     def _gather_buffer(self, rb, count, idx_t, seed, ctr, out):
         m, L = self.m, _lib.lib()

@@ -156,12 +156,17 @@ def ema_segment(p, start, end, target, rate, pack_map=None):
     return sg
 
 
+OPT_MAXSEG = 8   # segments per drpo_optim_step launch (csrc/optim.hip)
+
+
 def fused_step(segs):
-    """One drpo_optim_step launch over the given segments."""
+    """drpo_optim_step over the given segments: one launch per 8 segments."""
     from ._abi import OptimSeg
     L = _lib.lib()
-    arr = (OptimSeg * len(segs))(*segs)
-    _lib.check(L.drpo_optim_step(arr, len(segs), _lib.stream()), 'optim_step')
+    for k in range(0, len(segs), OPT_MAXSEG):
+        chunk = segs[k:k + OPT_MAXSEG]
+        arr = (OptimSeg * len(chunk))(*chunk)
+        _lib.check(L.drpo_optim_step(arr, len(chunk), _lib.stream()), 'optim_step')
 
 
 def grad_sumsq_multi(slices, outs):

@@ -77,6 +77,38 @@ def main():
     # the log-var bound term's gradient (+-0.01) is per-rank constant, so it averages to itself
     ref = torch.cat([g.reshape(-1) for g in full])
     assert torch.allclose(flat, ref, rtol=1e-4, atol=1e-6), float((flat - ref).abs().max())
+
+    # member-sharded fit (distributed.MemberShard): each rank differentiates only its
+    # members' NLL terms (+ the log-var bound term on rank 0); member gradients are
+    # the full-ensemble gradient's slices, the summed bound gradients its bound part
+    from drpo_amd.distributed import MemberShard
+    sh = MemberShard(E)
+    assert sh.ranges[-1][1] == E and sum(b_ - a_ for a_, b_ in sh.ranges) == E
+    Pm = {k: (v[sh.z0:sh.z1] if k in keys and k not in ('min_log_var', 'max_log_var') else v) for k, v in P.items()}
+    params = {k: Pm[k].detach().clone().requires_grad_(True) for k in keys}
+    Q = dict(Pm)
+    Q.update(params)
+    rows = torch.cat([torch.arange(z * b, (z + 1) * b) for z in range(sh.z0, sh.z1)])
+    loss = O.ens_compute_loss(Q, '', s[rows], a[rows], t[rows], sh.count) if sh.count else torch.zeros(())
+    if rank != 0:     # the oracle adds the bound term on every call; only rank 0 keeps it
+        loss = loss - 0.01 * (Q['max_log_var'].sum() - Q['min_log_var'].sum())
+    g = dict(zip(keys, torch.autograd.grad(loss, [params[k] for k in keys], allow_unused=True)))
+    for k, gf in zip(keys, full):
+        if k in ('min_log_var', 'max_log_var'):
+            gb = g[k].clone()
+            sh.sum_(gb)
+            assert torch.allclose(gb, gf, rtol=1e-4, atol=1e-6), (k, float((gb - gf).abs().max()))
+        else:
+            assert torch.allclose(g[k], gf[sh.z0:sh.z1], rtol=1e-4, atol=1e-6), k
+    # all-gather of member slices (uneven and even member counts) and holdout merge
+    for EE in (7, 8):
+        shx = MemberShard(EE)
+        w = torch.full((EE, 3, 2), -1.0)
+        w[shx.z0:shx.z1] = torch.arange(shx.z0, shx.z1, dtype=torch.float32).view(-1, 1, 1)
+        shx.gather_members_(w)
+        assert torch.equal(w, torch.arange(EE, dtype=torch.float32).view(-1, 1, 1).expand(EE, 3, 2))
+        mse = shx.merge_members(torch.arange(shx.z0, shx.z1, dtype=torch.float32) * 10, torch.zeros(EE))
+        assert torch.equal(mse, torch.arange(EE, dtype=torch.float32) * 10)
     dist.barrier()
     dist.destroy_process_group()
     print(f'rank {rank} ok')

@@ -40,3 +40,31 @@ def test_sac_data_parallel_two_ranks(tag):
         outs.append((p.returncode, out))
     for rc, out in outs:
         assert rc == 0, out[-3000:]
+
+
+def _run_ranks(script, args, world=2):
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY='0')
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, script)] + args, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out))
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+
+
+@pytest.mark.parametrize('env', ['quadrotor', 'tracking'])
+def test_member_sharded_fit_two_ranks(env):
+    """SURVEY §8(e) model fit: members sharded over 2 ranks reproduce the
+    single-process reference fit (all members, losses, elites) on every rank."""
+    _run_ranks('fit_shard_worker.py', [env])
