@@ -71,7 +71,7 @@ def synth_replay(S, A, C, N, rng):
                 dones=np.zeros(N, bool), violations=np.zeros(N, bool), constraint_values=h)
 
 
-def make_alg(dev, B, H, E, seed, cfg_json):
+def make_alg(dev, B, H, E, seed, cfg_json, extra=None):
     import drpo_amd
     from drpo_amd.envs import ShapeEnv
     cfg = drpo_amd.SMBPO.Config()
@@ -80,6 +80,8 @@ def make_alg(dev, B, H, E, seed, cfg_json):
                 'model_cfg': {'ensemble_size': E, 'num_elites': min(5, E)},
                 'sac_cfg': {'batch_size': B, 'qc_under_uncertainty': True, 'distributional_qc': True,
                             'mlp_multiplier': True}})
+    if extra:
+        cfg.update(extra)
     drpo_amd.set_seed(seed)
     alg = drpo_amd.SMBPO(cfg, lambda id=None: ShapeEnv('quadrotor'), None, 100, device=dev, noise_seed=seed)
     return alg

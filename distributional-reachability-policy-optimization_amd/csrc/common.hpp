@@ -58,10 +58,19 @@ __host__ __device__ inline int round_up(int x, int m) { return (x + m - 1) / m *
 // ds_read_b128 pattern (rows l&15, k-offset 4*(l>>4)) bank-conflict free.
 __host__ __device__ inline int lds_ld(int K) { return round_up(K, 64) + 8; }
 
+// sigmoid on the hardware transcendentals (v_exp_f32 + v_rcp_f32, ~1 ulp each): the
+// libm expf + IEEE division forms cost ~40 VALU ops per element, which in the MLP
+// epilogues (8-16 elements per lane per layer) made every swish layer of the
+// ensemble ~2k cycles slower than the same layer with ReLU (rollout stamps).
+// Saturates cleanly: x -> -inf gives rcp(inf) = 0, x -> +inf gives 1.
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+
 template <int ACT>
 __device__ __forceinline__ float act_fn(float x) {
   if constexpr (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
-  else if constexpr (ACT == ACT_SILU) return x / (1.f + expf(-x));
+  else if constexpr (ACT == ACT_SILU) return x * fast_sigmoid(x);
   else if constexpr (ACT == ACT_TANH) return tanhf(x);
   else return x;
 }
@@ -171,6 +180,22 @@ __device__ __forceinline__ void squashed_gaussian_row(RawAt raw_at, int64_t i, i
 #define DRPO_UNIFORM_WEIGHT_LOADS 0
 #endif
 
+// Load / store through a global (address space 1) pointer. Pointers that reach the
+// MLP cores as generic (rebuilt from SGPRs by uniform_ptr, or read from a device
+// descriptor) otherwise compile to FLAT accesses, which count against lgkmcnt as
+// well as vmcnt and complete out of order: every LDS wait then becomes
+// "s_waitcnt vmcnt(0) lgkmcnt(0)" and drains the whole weight prefetch ring
+// (rollout actor 256x256 layer: 12.9k -> 10.7k cycles per step with global loads).
+template <typename T>
+static __device__ __forceinline__ T gload(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)(p);
+}
+
+template <typename T>
+static __device__ __forceinline__ void gstore(T* p, T v) {
+  *(__attribute__((address_space(1))) T*)(p) = v;
+}
+
 static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
@@ -181,9 +206,9 @@ static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
 static __device__ __forceinline__ f32x4 load_pk(const float* __restrict__ P, int cb, int s, int NKS) {
   if constexpr (DRPO_UNIFORM_WEIGHT_LOADS) {
     const float* base = uniform_ptr(P) + ((size_t)__builtin_amdgcn_readfirstlane(cb * NKS + s) << 8);
-    return *reinterpret_cast<const f32x4*>(base + ((threadIdx.x & 63) << 2));
+    return gload(reinterpret_cast<const f32x4*>(base + ((threadIdx.x & 63) << 2)));
   } else {
-    return *reinterpret_cast<const f32x4*>(P + ((size_t)(cb * NKS + s) << 8) + ((threadIdx.x & 63) << 2));
+    return gload(reinterpret_cast<const f32x4*>(P + ((size_t)(cb * NKS + s) << 8) + ((threadIdx.x & 63) << 2)));
   }
 }
 
@@ -193,6 +218,16 @@ static __device__ __forceinline__ f32x4 load_pk(const float* __restrict__ P, int
 // wave per SIMD. The ring is indexed only by compile-time constants (unrolled),
 // so it stays in VGPRs.
 constexpr int PF_D = 4;
+
+// Ring depth of the unrolled (compile-time K) cores: deeper for waves that own few
+// column blocks (each k-step is then only 4*MAXC MFMAs of cover per wave)
+#ifndef DRPO_PF_SCALE
+#define DRPO_PF_SCALE 8
+#endif
+template <int MAXC>
+__host__ __device__ constexpr int pf_depth() {
+  return DRPO_PF_SCALE / MAXC > PF_D ? (DRPO_PF_SCALE / MAXC > 8 ? 8 : DRPO_PF_SCALE / MAXC) : PF_D;
+}
 
 // Optional global saves of the tile (rows < nrows only): gy = post-activation,
 // gz = pre-activation, row stride ldg (already offset to the tile's first row).
@@ -212,7 +247,7 @@ __device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N,
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int col = (wave + NW * c) * 16 + (lane & 15);
-    bv[c] = (bias && col < N) ? bias[col] : 0.f;
+    bv[c] = (bias && col < N) ? gload(bias + col) : 0.f;
   }
 }
 
@@ -237,8 +272,8 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
         if (col < N && row < gs.nrows) {
-          if (gs.gy) gs.gy[(size_t)row * gs.ldg + col] = y;
-          if (gs.gz) gs.gz[(size_t)row * gs.ldg + col] = z;
+          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -285,9 +320,10 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f32x4 bq[PF_D][MAXC];
+  constexpr int PF = NK > 0 ? pf_depth<MAXC>() : PF_D;
+  f32x4 bq[PF][MAXC];
 #pragma unroll
-  for (int u = 0; u < PF_D - 1; ++u)
+  for (int u = 0; u < PF - 1; ++u)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(P, cbs[c], min(u, NKS - 1), NKS);
   float bvs[MAXC];
@@ -299,9 +335,9 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
     for (int rb = 0; rb < RB; ++rb) an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
-      if (s + PF_D - 1 < NK) {
+      if (s + PF - 1 < NK) {
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) bq[(s + PF_D - 1) % PF_D][c] = load_pk(P, cbs[c], s + PF_D - 1, NKS);
+        for (int c = 0; c < MAXC; ++c) bq[(s + PF - 1) % PF][c] = load_pk(P, cbs[c], s + PF - 1, NKS);
       }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
@@ -319,7 +355,7 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
         for (int c = 0; c < MAXC; ++c)
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
-            acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF_D][c][m], acc[rb][c], 0, 0, 0);
+            acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF][c][m], acc[rb][c], 0, 0, 0);
     }
   } else {
     for (int kb = 0; kb < NKS; kb += PF_D) {
@@ -401,7 +437,7 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
   // each wave: at most ceil(16/NW) k-steps for K <= 256; issue all loads first
   constexpr int MAXS = (16 + NW - 1) / NW;
   f32x4 b[MAXS], a[MAXS][RB];
-  const float bias_v = (bias && (tid & 15) < N) ? bias[tid & 15] : 0.f;   // column (e & 15) == (tid & 15) below
+  const float bias_v = (bias && (tid & 15) < N) ? gload(bias + (tid & 15)) : 0.f;   // column (e & 15) == (tid & 15) below
 #pragma unroll
   for (int q = 0; q < MAXS; ++q) {
     const int s = wave + NW * q;
@@ -446,8 +482,8 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
     const int row = rb * 16 + rr;
     if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
     if (col < N && row < gs.nrows) {
-      if (gs.gy) gs.gy[(size_t)row * gs.ldg + col] = y;
-      if (gs.gz) gs.gz[(size_t)row * gs.ldg + col] = z;
+      if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+      if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
     }
   }
 }

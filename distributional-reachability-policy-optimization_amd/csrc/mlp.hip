@@ -339,7 +339,7 @@ __device__ __forceinline__ float act_grad(int act, float y, float z) {
     case ACT_RELU: return y > 0.f ? 1.f : 0.f;
     case ACT_TANH: return 1.f - y * y;
     case ACT_SILU: {
-      const float s = 1.f / (1.f + expf(-z));
+      const float s = fast_sigmoid(z);
       return s * (1.f + z * (1.f - s));
     }
     default: return 1.f;
@@ -369,9 +369,9 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__
         g = cur[r * LDH + k];
         if (act != ACT_NONE) {
           const size_t idx = so + (size_t)r * dout + k;
-          g *= act_grad(act, sy ? sy[idx] : 0.f, sz ? sz[idx] : 0.f);
+          g *= act_grad(act, sy ? gload(sy + idx) : 0.f, sz ? gload(sz + idx) : 0.f);
         }
-        if (dzp) dzp[so + (size_t)r * dout + k] = g;
+        if (dzp) gstore(dzp + so + (size_t)r * dout + k, g);
       }
       cur[r * LDH + k] = g;
     }
@@ -404,7 +404,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     const int wpad = round_up(w, 16);
     for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
       const int r = e / wpad, k = e - r * wpad;
-      dst[r * LDH + k] = (r < nrows && k < w) ? n.gout[((size_t)z * a.rows + row0 + r) * w + k] : 0.f;
+      dst[r * LDH + k] = (r < nrows && k < w) ? gload(n.gout + ((size_t)z * a.rows + row0 + r) * w + k) : 0.f;
     }
     __syncthreads();
   };
@@ -414,7 +414,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
       const int r = e / n.dx_cols, k = e - r * n.dx_cols;
       float* p = n.dx + ((size_t)z * a.rows + row0 + r) * n.dx_cols + k;
       const float v = src[r * LDH + n.dx_col0 + k];
-      *p = n.dx_accumulate ? *p + v : v;
+      gstore(p, n.dx_accumulate ? gload(p) + v : v);
     }
   };
 

@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #define DRPO_UNIFORM_WEIGHT_LOADS 1   // scalar-base weight loads (see load_pk)
+#define DRPO_PF_SCALE 12              // ring depth 6 for 2-block waves, 8 for 1-block waves
 #include "common.hpp"
 #include "env_constraints.hpp"
 
@@ -615,11 +616,13 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       tile_dense_narrow_pair<NW, RB, ACT_NONE>(h1, h3, ldh, Hm, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm, red);
     } else {
       lds_barrier();
+      if (t == 2) RSTAMP(7);
       tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
       lds_barrier();
       if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm, red);
       else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm);
       lds_barrier();
+      if (t == 2) RSTAMP(8);
       tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, lW1, lb1, Hm, h1, ldh);
       lds_barrier();
       if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm, red);

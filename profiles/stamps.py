@@ -95,11 +95,14 @@ def fused_stamps():
     L = _lib.lib()
     L.drpo_debug_stamps_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device('cuda')
-    alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON)
+    hm = int(os.environ.get('DRPO_STAMPS_HM', '200'))   # model width (200 = reference; else the unpaired path)
+    alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON, extra={'model_cfg': {'hidden_dim': hm}})
     rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)
+    if os.environ.get('DRPO_STAMPS_ONE_MEMBER'):      # every step on member 0 (L2-warm member weights)
+        alg.model_ensemble._elite_inds = [0]
     alg.rollout_engine = 2
     for _ in range(3):
         alg.rollout(alg.actor)
@@ -109,6 +112,8 @@ def fused_stamps():
     st = buf[:256].astype(np.int64)
     names = ['start', 'noise', 'actor L1', 'actor L2', 'actor L3', 'sample', 'member L1', 'member L2', 'pair L1',
              'pair L2', 'gauss', 'constraints', 'staging']
+    if hm != 200:
+        names[8:10] = ['diff L1+L2', 'lv L1+L2']
     print('== rollout_persist_kernel step t=2 (B=4096, quadrotor): cycles per phase, mean over 256 workgroups')
     tot = 0
     for c in range(1, 13):
