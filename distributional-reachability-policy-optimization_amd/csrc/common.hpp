@@ -423,6 +423,67 @@ __device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, cons
 // waves (k-steps s == wave mod NW), partial 16x16 tiles are summed through LDS
 // (`red`: NW*RB*256 floats), then bias + activation. Avoids one wave doing the
 // whole narrow head serially while the others idle.
+//
+// tile_dense_narrow_partials stops after the hand-off: the value of (row, col) is
+// narrow_sum<NW, RB>(red, row, col) + bias[col], summed in the same order as
+// tile_dense_narrow's epilogue (callers fuse their own elementwise work there).
+template <int NW, int RB>
+__device__ __forceinline__ float narrow_sum(const float* red, int row, int col) {
+  const int rb = row >> 4, rr = row & 15;
+  float v = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) v += red[(w * RB + rb) * 256 + rr * 16 + col];
+  return v;
+}
+
+template <int NW, int RB>
+__device__ __forceinline__ void tile_dense_narrow_partials(const float* in, int ldi, int K,
+                                                           const float* __restrict__ P, float* red) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NKS = (K + 15) >> 4;
+  f32x4 acc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int MAXS = (16 + NW - 1) / NW;
+  f32x4 b[MAXS], a[MAXS][RB];
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    const int s = wave + NW * q;
+    const int sc = s < NKS ? s : 0;
+    b[q] = load_pk(P, 0, sc, NKS);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + sc * 16 + 4 * g);
+  }
+  for (int kb = NW * MAXS; kb < NKS; kb += NW) {
+    if (kb + wave < NKS) {
+      const f32x4 bb = load_pk(P, 0, kb + wave, NKS);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const f32x4 aa = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + (kb + wave) * 16 + 4 * g);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[m], bb[m], acc[rb], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    if (wave + NW * q < NKS) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][rb][m], b[q][m], acc[rb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+  lds_barrier();
+}
+
 template <int NW, int RB, int ACT>
 __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int K, const float* __restrict__ P,
                                                   const float* __restrict__ bias, int N, float* out, int ldo,
@@ -588,6 +649,62 @@ __device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K,
   const int NCB = ((N1 + 15) >> 4) + ((N2 + 15) >> 4);
   const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
   tile_dense_pair_nc<NW, RB, MAXC, ACT, NK>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
+}
+
+// Partials-only form of tile_dense_narrow_pair (below): the value of layer `which`
+// at (row, col) is narrow_pair_sum<NW, RB>(red, which, row, col) + its bias, in the
+// same summation order as tile_dense_narrow_pair's epilogue.
+template <int NW, int RB>
+__device__ __forceinline__ float narrow_pair_sum(const float* red, int which, int row, int col) {
+  constexpr int HW = NW / 2;
+  const int rb = row >> 4, rr = row & 15;
+  float v = 0.f;
+#pragma unroll
+  for (int w = 0; w < HW; ++w) v += red[((which * HW + w) * RB + rb) * 256 + rr * 16 + col];
+  return v;
+}
+
+template <int NW, int RB>
+__device__ __forceinline__ void tile_dense_narrow_pair_partials(const float* in1, const float* in2, int ldi, int K,
+                                                                const float* __restrict__ P1,
+                                                                const float* __restrict__ P2, float* red) {
+  constexpr int HW = NW / 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NKS = (K + 15) >> 4;
+  const bool second = wave >= HW;
+  const int wl = second ? wave - HW : wave;
+  const float* P = second ? P2 : P1;
+  const float* in = second ? in2 : in1;
+  f32x4 acc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int MAXS = (16 + HW - 1) / HW;      // K <= 256
+  f32x4 b[MAXS], a[MAXS][RB];
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    const int s = wl + HW * q;
+    const int sc = s < NKS ? s : 0;
+    b[q] = load_pk(P, 0, sc, NKS);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + sc * 16 + 4 * g);
+  }
+#pragma unroll
+  for (int q = 0; q < MAXS; ++q) {
+    if (wl + HW * q < NKS) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][rb][m], b[q][m], acc[rb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+  lds_barrier();
 }
 
 // Two narrow layers (N1, N2 <= 16) on two input tiles at once: waves [0, NW/2) split

@@ -92,7 +92,7 @@ __device__ __forceinline__ float* run_net(const drpo_mlp_fwd_t& a, float* in, fl
     if (l < a.net[NI].nl) {
       float* out = (cur == bufA) ? bufB : bufA;
       run_layer(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red);
-      __syncthreads();
+      lds_barrier();
       STAMP(2 + 4 * NI + l);
       cur = out;
     }
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
     }
     xin[r * LDH + k] = v;
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(1);
   if (!a.trunk) {
     if (blockIdx.y == 0) run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
       const int r = e / wpad, k = e - r * wpad;
       T[r * LDH + k] = t[r * LDH + k];
     }
-    __syncthreads();
+    lds_barrier();
     if (a.nnets > 1) run_net<1>(a, T, bA, bB, z, row0, nrows, red);
     if (a.nnets > 2) run_net<2>(a, T, bA, bB, z, row0, nrows, red);
   }
@@ -195,7 +195,7 @@ __device__ __forceinline__ float* run_net_g(const drpo_mlp_fwd_t* __restrict__ a
   for (int l = 0; l < nl; ++l) {
     float* out = (cur == bufA) ? bufB : bufA;
     run_layer<RB>(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
-    __syncthreads();
+    lds_barrier();
     cur = out;
   }
   return cur;
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
     }
     xin[r * LDH + k] = v;
   }
-  __syncthreads();
+  lds_barrier();
   float* outp;
   if (!a->trunk) {
     outp = run_net_g<RB>(a, net, xin, bA, bB, z, row0, nrows, red);
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
       const int r = e / wpad, k = e - r * wpad;
       T[r * LDH + k] = t[r * LDH + k];
     }
-    __syncthreads();
+    lds_barrier();
     outp = nullptr;
     for (int h = 1; h < a->nnets; ++h) run_net_g<RB>(a, h, T, bA, bB, z, row0, nrows, red);
   }
@@ -375,12 +375,12 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__
       }
       cur[r * LDH + k] = g;
     }
-    __syncthreads();
+    lds_barrier();
     if (l == 0 && !need_dx0) return nullptr;   // input gradient not wanted: dZ_0 (saved) is all wgrad needs
     float* out = (cur == bA) ? bB : bA;
     // dY_prev = dZ W: transposed mirror, N = din, K = dout
     tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, dout, W, nullptr, din, out, LDH);
-    __syncthreads();
+    lds_barrier();
     cur = out;
   }
   return cur;
@@ -406,7 +406,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
       const int r = e / wpad, k = e - r * wpad;
       dst[r * LDH + k] = (r < nrows && k < w) ? gload(n.gout + ((size_t)z * a.rows + row0 + r) * w + k) : 0.f;
     }
-    __syncthreads();
+    lds_barrier();
   };
   auto store_dx = [&](const drpo_mlp_bwd_net_t& n, const float* src) {
     if (!n.dx) return;
@@ -428,7 +428,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
   const int tw = a.net[0].L[a.net[0].nl - 1].dout;
   const int twpad = round_up(tw, 16);
   for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) DT[(e / twpad) * LDH + e % twpad] = 0.f;
-  __syncthreads();
+  lds_barrier();
   for (int h = 1; h < a.nnets; ++h) {
     load_gout(a.net[h], G);
     const float* gh = bwd_net(a.net[h], G, bA, bB, z, a.rows, row0, nrows, true);
@@ -436,7 +436,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
       const int r = e / twpad, k = e - r * twpad;
       DT[r * LDH + k] += gh[r * LDH + k];
     }
-    __syncthreads();
+    lds_barrier();
   }
   const float* gx = bwd_net(a.net[0], DT, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
   if (gx) store_dx(a.net[0], gx);

@@ -227,28 +227,51 @@ struct OptimArgs {
   int n;
 };
 
-__device__ __forceinline__ void pack_write(const drpo_pack_map_t* mp, int64_t i, float pv, float tv, bool has_t) {
-  // find the weight matrix containing flat index i (<= 16 entries, uniform per block mostly)
-  for (int l = 0; l < mp->nlayers; ++l) {
-    const int din = mp->din[l], dout = mp->dout[l];
-    const int msz = din * dout;                       // group tensors are < 2^31 floats
-    const int64_t rel64 = i - mp->off[l];
-    if (rel64 < 0 || rel64 >= (int64_t)msz * mp->nbatch[l]) continue;
-    const int rel = (int)rel64;
-    const int z = rel / msz;
-    const int w = rel - z * msz;
-    const int o = w / din, k = w - o * din;
-    const int ncb = (dout + 15) >> 4, nks = (din + 15) >> 4;
+// Packed-mirror refresh for the n (<= 4) consecutive flat elements i0.. of one thread.
+// The weight matrix holding i0 is found once; the (member, row, column) coordinates
+// are divided out once and then stepped (consecutive elements are consecutive
+// columns), so the per-element cost is a few integer adds instead of two 32-bit
+// divisions and a layer search.
+__device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i0, int n, const float (&pv)[4],
+                                            const float (&tv)[4], bool has_t) {
+  // Every tensor of a flat group starts 64-float aligned (params.py) and i0 is a
+  // multiple of 4 whenever n > 1, so the n elements never reach into a second weight
+  // matrix: past the end of the one holding i0 lies bias or padding.
+  const int nl = mp->nlayers;
+  int l = 0;
+  int64_t rel64 = 0;
+  for (; l < nl; ++l) {
+    rel64 = i0 - mp->off[l];
+    if (rel64 >= 0 && rel64 < (int64_t)mp->din[l] * mp->dout[l] * mp->nbatch[l]) break;
+  }
+  if (l == nl) return;
+  const int din = mp->din[l], dout = mp->dout[l], nb = mp->nbatch[l];
+  const int msz = din * dout;                         // group tensors are < 2^31 floats
+  const int rel = (int)rel64;
+  int z = rel / msz;
+  const int w = rel - z * msz;
+  int o = w / din, k = w - o * din;
+  const int ncb = (dout + 15) >> 4, nks = (din + 15) >> 4;
+  float* P = mp->P;
+  float* Pt = has_t ? mp->Pt : nullptr;
+  float* PT = mp->PT;
+  for (int e = 0; e < n; ++e) {
     const int64_t base = mp->poff[l] + (int64_t)z * ncb * nks * 256;
     // forward mirror: fragment (o>>4, k>>4), lane ((k>>2)&3)*16 + (o&15), component k&3
     const int64_t pi = base + ((int64_t)((o >> 4) * nks + (k >> 4)) << 8) + ((((k >> 2) & 3) * 16 + (o & 15)) << 2) + (k & 3);
-    if (mp->P) mp->P[pi] = pv;
-    if (has_t && mp->Pt) mp->Pt[pi] = tv;
-    if (mp->PT) {   // transposed mirror: fragment (k>>4, o>>4), lane ((o>>2)&3)*16 + (k&15), component o&3
+    if (P) P[pi] = pv[e];
+    if (Pt) Pt[pi] = tv[e];
+    if (PT) {   // transposed mirror: fragment (k>>4, o>>4), lane ((o>>2)&3)*16 + (k&15), component o&3
       const int64_t ti = base + ((int64_t)((k >> 4) * ncb + (o >> 4)) << 8) + ((((o >> 2) & 3) * 16 + (k & 15)) << 2) + (o & 3);
-      mp->PT[ti] = pv;
+      PT[ti] = pv[e];
     }
-    return;
+    if (++k == din) {
+      k = 0;
+      if (++o == dout) {
+        o = 0;
+        if (++z == nb) return;
+      }
+    }
   }
 }
 
@@ -273,26 +296,69 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   const float coef = S.partial ? s_coef : 1.f;
   const int64_t e0 = S.start + (bid - a.first[q]) * OPT_BLOCK_ELEMS;
   const int64_t e1 = min(S.end, e0 + OPT_BLOCK_ELEMS);
-  for (int64_t i = e0 + threadIdx.x; i < e1; i += 256) {
-    float p = S.p[i];
-    if (S.adam) {
-      float g = S.g[i] * coef;
-      if (S.weight_decay != 0.f) g = fmaf(p, S.weight_decay, g);
-      const float m = torch_lerp(S.m[i], g, 1.f - S.beta1);
-      const float v = fmaf(S.v[i], S.beta2, (1.f - S.beta2) * g * g);
-      S.m[i] = m;
-      S.v[i] = v;
-      const float denom = sqrtf(v) / S.bc2_sqrt + S.eps;
-      p = p - S.lr_over_bc1 * (m / denom);
-      S.p[i] = p;
+  // Each thread owns 4 consecutive elements: all of its loads are issued before any
+  // arithmetic (one 16-byte load per array when the segment start is 4-aligned), so
+  // a block waits one memory latency instead of one per element.
+  const int64_t i0 = e0 + 4 * (int64_t)threadIdx.x;
+  if (i0 >= e1) return;
+  const int n = (int)min((int64_t)4, e1 - i0);
+  const bool vec = n == 4 && (S.start & 3) == 0;
+  float p[4], g[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f}, v[4] = {0.f, 0.f, 0.f, 0.f};
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  auto ld4 = [&](const float* src, float (&dst)[4]) {
+    if (vec) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(src + i0);
+      dst[0] = x[0]; dst[1] = x[1]; dst[2] = x[2]; dst[3] = x[3];
+    } else {
+      for (int e = 0; e < n; ++e) dst[e] = src[i0 + e];
     }
-    if (S.zero_grad) S.g[i] = 0.f;
-    float t = 0.f;
-    if (S.ema_target) {
-      t = S.ema_rate * p + S.ema_keep * S.ema_target[i];
-      S.ema_target[i] = t;
+  };
+  auto st4 = [&](float* dst, const float (&src)[4]) {
+    if (vec) {
+      *reinterpret_cast<f32x4*>(dst + i0) = f32x4{src[0], src[1], src[2], src[3]};
+    } else {
+      for (int e = 0; e < n; ++e) dst[i0 + e] = src[e];
     }
-    if (S.map) pack_write(S.map, i, p, t, S.ema_target != nullptr);
+  };
+  ld4(S.p, p);
+  if (S.adam) {
+    ld4(S.g, g);
+    ld4(S.m, m);
+    ld4(S.v, v);
+  }
+  if (S.ema_target) ld4(S.ema_target, t);
+  if (S.adam) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float ge = g[e] * coef;
+      if (S.weight_decay != 0.f) ge = fmaf(p[e], S.weight_decay, ge);
+      m[e] = torch_lerp(m[e], ge, 1.f - S.beta1);
+      v[e] = fmaf(v[e], S.beta2, (1.f - S.beta2) * ge * ge);
+      const float denom = sqrtf(v[e]) / S.bc2_sqrt + S.eps;
+      p[e] = p[e] - S.lr_over_bc1 * (m[e] / denom);
+    }
+    st4(S.m, m);
+    st4(S.v, v);
+    st4(S.p, p);
+  }
+  if (S.zero_grad) {
+    const float zz[4] = {0.f, 0.f, 0.f, 0.f};
+    st4(S.g, zz);
+  }
+  if (S.ema_target) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[e] = S.ema_rate * p[e] + S.ema_keep * t[e];
+    st4(S.ema_target, t);
+  }
+  if (S.map) {
+    if (vec) {
+      pack_write4(S.map, i0, 4, p, t, S.ema_target != nullptr);
+    } else {
+      for (int e = 0; e < n; ++e) {
+        const float pe[4] = {p[e], 0.f, 0.f, 0.f}, te[4] = {t[e], 0.f, 0.f, 0.f};
+        pack_write4(S.map, i0 + e, 1, pe, te, S.ema_target != nullptr);
+      }
+    }
   }
 }
 

@@ -575,6 +575,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
 
     if (t == 2) RSTAMP(0);
     if (t == 2) RSTAMP(1);
+    // alive flags of this step's rows / of the next step's (double-buffered: the
+    // constraint wave writes the next step's while the staging waves read these)
+    int* alive_cur = (t & 1) ? flags : alive;
+    int* alive_nxt = (t & 1) ? alive : flags;
     // ---- actor MLP (src/policy.py:61-100) ------------------------------------
     tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh);
     lds_barrier();
@@ -582,122 +586,138 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(3);
-    tile_dense_narrow<NW, RB, ACT_NONE>(h2, ldh, Ha, step_opaque(p.aW3), step_opaque(p.ab3), 2 * A, ao, 20, red);
+    // ---- actor head + squashed Gaussian sample + model input [normalize(s), a]:
+    //      the head's split-K partials are reduced by the threads that sample
+    //      (one thread per (row, action dim) sums the mu and log-std columns) ----
+    {
+      const float* ab3 = step_opaque(p.ab3);
+      float bmu = 0.f, braw = 0.f;
+      if (tid < ROWS * A) {   // ROWS * A <= NT (A <= 8)
+        const int d = tid % A;
+        bmu = gload(ab3 + d);
+        braw = gload(ab3 + A + d);
+      }
+      tile_dense_narrow_partials<NW, RB>(h2, ldh, Ha, step_opaque(p.aW3), red);
+      if (tid < ROWS * A) {
+        const int r = tid / A, d = tid - r * A;
+        const float mu = narrow_sum<NW, RB>(red, r, d) + bmu;
+        const float raw = narrow_sum<NW, RB>(red, r, A + d) + braw;
+        const float ls = -6.f + 10.f * sigmoidf(raw);
+        const float a = tanhf(nz_a[r * 8 + d] * expf(ls) + mu);
+        act[r * 8 + d] = a;
+        xin[r * ldx + S + d] = a;
+      }
+      for (int e = tid; e < ROWS * S; e += NT) {
+        const int r = e / S, k = e - r * S;
+        xin[r * ldx + k] = (sraw[r * ldss + k] - v_nm[k]) / v_ns[k];
+      }
+    }
     lds_barrier();
     if (t == 2) RSTAMP(4);
-
-    // ---- squashed Gaussian sample + model input [normalize(s), a] -------------
-    for (int e = tid; e < ROWS * A; e += NT) {
-      const int r = e / A, d = e - r * A;
-      const float mu = ao[r * 20 + d], raw = ao[r * 20 + A + d];
-      const float ls = -6.f + 10.f * sigmoidf(raw);
-      const float a = tanhf(nz_a[r * 8 + d] * expf(ls) + mu);
-      act[r * 8 + d] = a;
-      xin[r * ldx + S + d] = a;
-    }
-    for (int e = tid; e < ROWS * S; e += NT) {
-      const int r = e / S, k = e - r * S;
-      xin[r * ldx + k] = (sraw[r * ldss + k] - v_nm[k]) / v_ns[k];
-    }
-    lds_barrier();
-    if (t == 2) RSTAMP(5);
 
     // ---- elite member forward (src/dynamics.py:112-122) -----------------------
     tile_dense<NW, RB, MAXC, ACT_SILU>(xin, ldx, S + A, mW1, mb1, Hm, h1, ldh);
     lds_barrier();
-    if (t == 2) RSTAMP(6);
+    if (t == 2) RSTAMP(5);
     tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, mW2, mb2, Hm, h2, ldh);
+    lds_barrier();
+    if (t == 2) RSTAMP(6);
     if (paired) {
-      lds_barrier();
-      if (t == 2) RSTAMP(7);
       tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
       lds_barrier();
-      if (t == 2) RSTAMP(8);
-      tile_dense_narrow_pair<NW, RB, ACT_NONE>(h1, h3, ldh, Hm, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm, red);
-    } else {
-      lds_barrier();
       if (t == 2) RSTAMP(7);
+      // output heads (split-K partials) reduced by the threads that form the
+      // residual mean, soft-clamp the log-variance and sample the next state
+      float bd = 0.f, bl = 0.f;
+      if (tid < ROWS * S1) {   // ROWS * S1 <= NT (S1 <= 16)
+        const int j = tid % S1;
+        bd = gload(db2 + j);
+        bl = gload(lb2 + j);
+      }
+      tile_dense_narrow_pair_partials<NW, RB>(h1, h3, ldh, Hm, dW2, lW2, red);
+      if (tid < ROWS * S1) {
+        const int r = tid / S1, j = tid - r * S1;
+        const float mean = (narrow_pair_sum<NW, RB>(red, 0, r, j) + bd) + (j < S ? sraw[r * ldss + j] : 0.f);
+        float lv = narrow_pair_sum<NW, RB>(red, 1, r, j) + bl;
+        lv = v_hi[j] - softplusf(v_hi[j] - lv);
+        lv = v_lo[j] + softplusf(lv - v_lo[j]);
+        const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
+        if (j < S) xin[r * ldx + j] = x;
+        else rew[r] = x;
+      }
+    } else {
       tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
       lds_barrier();
       if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm, red);
       else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm);
       lds_barrier();
-      if (t == 2) RSTAMP(8);
       tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, lW1, lb1, Hm, h1, ldh);
       lds_barrier();
+      if (t == 2) RSTAMP(7);
       if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm, red);
       else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm);
+      lds_barrier();
+      // residual mean, log-var soft clamp, Gaussian sample
+      for (int e = tid; e < ROWS * S1; e += NT) {
+        const int r = e / S1, j = e - r * S1;
+        const float mean = dout[r * ldm + j] + (j < S ? sraw[r * ldss + j] : 0.f);
+        float lv = lout[r * ldm + j];
+        lv = v_hi[j] - softplusf(v_hi[j] - lv);
+        lv = v_lo[j] + softplusf(lv - v_lo[j]);
+        const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
+        if (j < S) xin[r * ldx + j] = x;
+        else rew[r] = x;
+      }
     }
     lds_barrier();
-    if (t == 2) RSTAMP(9);
+    if (t == 2) RSTAMP(8);
 
-    // ---- residual mean, log-var soft clamp, Gaussian sample -------------------
-    for (int e = tid; e < ROWS * S1; e += NT) {
-      const int r = e / S1, j = e - r * S1;
-      const float mean = dout[r * ldm + j] + (j < S ? sraw[r * ldss + j] : 0.f);
-      float lv = lout[r * ldm + j];
-      lv = v_hi[j] - softplusf(v_hi[j] - lv);
-      lv = v_lo[j] + softplusf(lv - v_lo[j]);
-      const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
-      if (j < S) xin[r * ldx + j] = x;
-      else rew[r] = x;
-    }
-    lds_barrier();
-    if (t == 2) RSTAMP(10);
-
-    // ---- constraints, alive map of this step (wave 0); the other waves draw the
-    //      next step's noise meanwhile (this step's draws were consumed above) ----
-    if (t + 1 < p.H)
-      persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, A, S1, B, t + 1, row0, nrows, nz_a, nz_m, 64, NT - 64);
+    // ---- one phase: constraints + alive map + their staging writes (wave 0, one
+    //      lane per row), the states / actions staging writes and the state
+    //      hand-off (waves 1 .. NW/2-1), the next step's draws (waves NW/2 ..) ----
+    const size_t sb = (size_t)t * B + row0;
     if (tid < 64) {
       bool in_r = false, dn = false, vl = false;
-      if (tid < ROWS && alive[tid]) {
+      if (tid < ROWS && alive_cur[tid]) {
         float hh[8];
         env_constraints_row(p.env, xin + tid * ldx, dn, vl, hh);
-        for (int c = 0; c < C; ++c) hval[tid * 8 + c] = hh[c];
+        for (int c = 0; c < C; ++c) p.st_h[(sb + tid) * C + c] = hh[c];
+        p.st_r[sb + tid] = rew[tid];
+        p.st_dv[sb + tid] = (uint8_t)((dn ? 1 : 0) | (vl ? 2 : 0));
         in_r = true;
       }
-      if (tid < ROWS) flags[tid] = (dn ? 1 : 0) | (vl ? 2 : 0) | (in_r ? 4 : 0);   // bit2: row in this step
       const uint64_t mk = __ballot(in_r);
       if (in_r) p.inv[((size_t)t * p.ntiles + tile) * ROWS + __popcll(mk & ((1ull << tid) - 1ull))] = tid;
       if (tid == 0) p.cnt[(size_t)t * p.ntiles + tile] = __popcll(mk);
       const uint64_t still = __ballot(in_r && !dn);
-      if (tid < ROWS) alive[tid] = in_r && !dn;
+      if (tid < ROWS) alive_nxt[tid] = in_r && !dn;
       if (tid == 0) *s_nalive = __popcll(still);
+    } else if (tid < NT / 2) {
+      constexpr int NS = NT / 2 - 64;
+      const int ts = tid - 64;
+      for (int e = ts; e < ROWS * S; e += NS) {
+        const int r = e / S, k = e - r * S;
+        const float x = xin[r * ldx + k];
+        if (alive_cur[r]) {
+          p.st_s[(sb + r) * S + k] = sraw[r * ldss + k];
+          p.st_s2[(sb + r) * S + k] = x;
+        }
+        sraw[r * ldss + k] = x;   // same element, same thread
+      }
+      for (int e = ts; e < nrows * A; e += NS) {
+        const int r = e / A, d = e - r * A;
+        if (alive_cur[r]) p.st_a[(sb + r) * A + d] = act[r * 8 + d];
+      }
+    } else if (t + 1 < p.H) {
+      persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, A, S1, B, t + 1, row0, nrows, nz_a, nz_m, NT / 2, NT / 2);
     }
     lds_barrier();
-    if (t == 2) RSTAMP(11);
-
-    // ---- staging writes (this step's surviving rows), next step's states -------
-    const size_t sb = (size_t)t * B + row0;
-    for (int e = tid; e < ROWS * S; e += NT) {
-      const int r = e / S, k = e - r * S;
-      const float x = xin[r * ldx + k];
-      if (flags[r] & 4) {
-        p.st_s[(sb + r) * S + k] = sraw[r * ldss + k];
-        p.st_s2[(sb + r) * S + k] = x;
-      }
-      sraw[r * ldss + k] = x;   // same element, same thread: no barrier needed
-    }
-    for (int e = tid; e < nrows * A; e += NT) {
-      const int r = e / A, d = e - r * A;
-      if (flags[r] & 4) p.st_a[(sb + r) * A + d] = act[r * 8 + d];
-    }
-    for (int e = tid; e < nrows * C; e += NT) {
-      const int r = e / C, c = e - r * C;
-      if (flags[r] & 4) p.st_h[(sb + r) * C + c] = hval[r * 8 + c];
-    }
-    if (tid < nrows && (flags[tid] & 4)) {
-      p.st_r[sb + tid] = rew[tid];
-      p.st_dv[sb + tid] = (uint8_t)(flags[tid] & 3);
-    }
-    if (t == 2) RSTAMP(12);
+    if (t == 2) RSTAMP(9);
     const int n_alive = __builtin_amdgcn_readfirstlane(*s_nalive);   // uniform exit
     if (n_alive == 0) {   // the whole tile finished: later steps see no rows from it
       for (int t2 = t + 1 + tid; t2 < p.H; t2 += NT) p.cnt[(size_t)t2 * p.ntiles + tile] = 0;
       return;
     }
-    lds_barrier();
   }
 }
 
@@ -888,15 +908,21 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   a.lds = round_up(S, 4);
   for (int t = 0; t < H; ++t) a.members[t] = d->members[t];
 
-  constexpr int NW = 8;
+  static const int NW = [] {
+    const char* e = getenv("DRPO_ROLLOUT_NW");
+    return (e && atoi(e) == 16) ? 16 : 8;
+  }();
+  const int nw = rpt == 32 ? 8 : NW;
   const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 3 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 8 +
-                                                           64 + 2) + 4 + (size_t)NW * (rpt / 16) * 256 + 256);
+                                                           64 + 2) + 4 + (size_t)nw * (rpt / 16) * 256 + 256);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
   if (rpt == 32)
-    rollout_persist_kernel<2, NW><<<a.ntiles, NW * 64, lds_bytes, stream>>>(a);
+    rollout_persist_kernel<2, 8><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+  else if (NW == 16)
+    rollout_persist_kernel<1, 16><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);
   else
-    rollout_persist_kernel<1, NW><<<a.ntiles, NW * 64, lds_bytes, stream>>>(a);
+    rollout_persist_kernel<1, 8><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   DRPO_LAUNCH_CHECK("rollout_persist");
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[1], stream);
   rollout_scan_kernel<<<H, 256, 0, stream>>>(a.cnt, pos, n, a.ntiles);

@@ -110,13 +110,13 @@ def fused_stamps():
     buf = np.zeros((1 << 14, 16), np.uint64)
     L.drpo_debug_stamps_rollout(buf.ctypes.data, 256)
     st = buf[:256].astype(np.int64)
-    names = ['start', 'noise', 'actor L1', 'actor L2', 'actor L3', 'sample', 'member L1', 'member L2', 'pair L1',
-             'pair L2', 'gauss', 'constraints', 'staging']
+    names = ['start', 'noise', 'actor L1', 'actor L2', 'actor L3+sample', 'member L1', 'member L2', 'pair L1',
+             'pair L2+gauss', 'constr+staging']
     if hm != 200:
-        names[8:10] = ['diff L1+L2', 'lv L1+L2']
+        names[7:9] = ['diff L1+L2, lv L1', 'lv L2, gauss']
     print('== rollout_persist_kernel step t=2 (B=4096, quadrotor): cycles per phase, mean over 256 workgroups')
     tot = 0
-    for c in range(1, 13):
+    for c in range(1, len(names)):
         d = st[:, c] - st[:, c - 1]
         tot += d.mean()
         print(f'   {names[c]:12s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f}')
