@@ -302,10 +302,21 @@ __device__ __forceinline__ void lds_barrier() {
 
 // Core of tile_dense_impl for a wave that owns exactly MAXC valid column blocks
 // (the dispatcher below picks the instantiation per wave).
-template <int NW, int RB, int MAXC, int ACT, int NK>
+// NL > 0 (unrolled cores only): the first NL k-steps of every column block are read
+// from an LDS copy Pl of the packed mirror, laid out [cb][NL][256] (weights that stay
+// the same across the calls of a persistent kernel: fewer bytes per MFMA from L2).
+template <int NL>
+__device__ __forceinline__ f32x4 load_frag(const float* __restrict__ P, const float* Pl, int cb, int s, int NKS) {
+  if (s < NL)
+    return *(const __attribute__((address_space(3))) f32x4*)(Pl + ((cb * NL + s) << 8) + ((threadIdx.x & 63) << 2));
+  return load_pk(P, cb, s, NKS);
+}
+
+template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0>
 __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,
-                                                const GSave& gs) {
+                                                const GSave& gs, const float* Pl = nullptr) {
+  static_assert(NL == 0 || NK > 0, "LDS-resident k-steps need the unrolled core");
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -325,7 +336,7 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
 #pragma unroll
   for (int u = 0; u < PF - 1; ++u)
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(P, cbs[c], min(u, NKS - 1), NKS);
+    for (int c = 0; c < MAXC; ++c) bq[u][c] = load_frag<NL>(P, Pl, cbs[c], min(u, NKS - 1), NKS);
   float bvs[MAXC];
   load_bias<NW, MAXC>(bias, N, bvs);
 
@@ -337,7 +348,7 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
     for (int s = 0; s < NK; ++s) {
       if (s + PF - 1 < NK) {
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) bq[(s + PF - 1) % PF][c] = load_pk(P, cbs[c], s + PF - 1, NKS);
+        for (int c = 0; c < MAXC; ++c) bq[(s + PF - 1) % PF][c] = load_frag<NL>(P, Pl, cbs[c], s + PF - 1, NKS);
       }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
@@ -388,22 +399,23 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
 // blocks of a 200-wide layer on 8 waves) the waves own different counts, and each
 // runs the instantiation for its own count, so no wave loads or multiplies a
 // padding block (the branch is wave-uniform).
-template <int NW, int RB, int NC, int ACT, int NK>
+template <int NW, int RB, int NC, int ACT, int NK, int NL = 0>
 __device__ __forceinline__ void tile_dense_nc(int nc, const float* in, int ldi, int K, const float* __restrict__ P,
                                               const float* __restrict__ bias, int N, float* out, int ldo,
-                                              const GSave& gs) {
-  if (nc == NC) tile_dense_core<NW, RB, NC, ACT, NK>(in, ldi, K, P, bias, N, out, ldo, gs);
-  else if constexpr (NC > 1) tile_dense_nc<NW, RB, NC - 1, ACT, NK>(nc, in, ldi, K, P, bias, N, out, ldo, gs);
+                                              const GSave& gs, const float* Pl = nullptr) {
+  if (nc == NC) tile_dense_core<NW, RB, NC, ACT, NK, NL>(in, ldi, K, P, bias, N, out, ldo, gs, Pl);
+  else if constexpr (NC > 1) tile_dense_nc<NW, RB, NC - 1, ACT, NK, NL>(nc, in, ldi, K, P, bias, N, out, ldo, gs, Pl);
 }
 
-template <int NW, int RB, int MAXC, int ACT, int NK>
+template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0>
 __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,
-                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0},
+                                                const float* Pl = nullptr) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NCB = (N + 15) >> 4;
   const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
-  tile_dense_nc<NW, RB, MAXC, ACT, NK>(nc, in, ldi, K, P, bias, N, out, ldo, gs);
+  tile_dense_nc<NW, RB, MAXC, ACT, NK, NL>(nc, in, ldi, K, P, bias, N, out, ldo, gs, Pl);
 }
 
 // K (input width) -> compile-time k-step count for the widths on the path
@@ -436,9 +448,10 @@ __device__ __forceinline__ float narrow_sum(const float* red, int row, int col) 
   return v;
 }
 
-template <int NW, int RB>
+template <int NW, int RB, bool LDSW = false>
 __device__ __forceinline__ void tile_dense_narrow_partials(const float* in, int ldi, int K,
-                                                           const float* __restrict__ P, float* red) {
+                                                           const float* __restrict__ P, float* red,
+                                                           const float* Pl = nullptr) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -452,13 +465,13 @@ __device__ __forceinline__ void tile_dense_narrow_partials(const float* in, int 
   for (int q = 0; q < MAXS; ++q) {
     const int s = wave + NW * q;
     const int sc = s < NKS ? s : 0;
-    b[q] = load_pk(P, 0, sc, NKS);
+    b[q] = LDSW ? load_frag<16>(P, Pl, 0, sc, 16) : load_pk(P, 0, sc, NKS);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) a[q][rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + sc * 16 + 4 * g);
   }
   for (int kb = NW * MAXS; kb < NKS; kb += NW) {
     if (kb + wave < NKS) {
-      const f32x4 bb = load_pk(P, 0, kb + wave, NKS);
+      const f32x4 bb = load_pk(P, 0, kb + wave, NKS);   // K > 256 (never LDS-resident)
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const f32x4 aa = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + (kb + wave) * 16 + 4 * g);

@@ -482,7 +482,14 @@ __device__ __forceinline__ void persist_noise(const float* eps_a, const float* e
   }
 }
 
-template <int RB, int NW>
+// LW: the actor's first layer, its output head and the first PERSIST_L2_LDS k-steps of
+// its hidden layer stay in LDS for the whole launch (the actor is the same every
+// step; with one 16-row tile per CU every weight byte is otherwise re-read from L2
+// each step, and the layers run at the CU's L2 read rate). Needs S <= 16,
+// Ha == 256, 2A <= 16 and the LDS to spare (host check).
+constexpr int PERSIST_L2_LDS = 3;
+
+template <int RB, int NW, bool LW>
 __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p) {
   constexpr int ROWS = RB * 16;
   constexpr int NT = NW * 64;
@@ -518,6 +525,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   float* v_ns = vecs + 64;                                                                    \
   float* v_lo = vecs + 128;                                                                   \
   float* v_hi = vecs + 192;                                                                   \
+  float* wl1 = vecs + 256;                  /* LW: actor L1 mirror [16 cb][256] */               \
+  float* wl3 = wl1 + 16 * 256;              /* LW: actor head mirror [16 k-steps][256] */        \
+  float* wl2 = wl3 + 16 * 256;              /* LW: actor L2 [16 cb][PERSIST_L2_LDS][256] */      \
+  (void)wl1; (void)wl2; (void)wl3;                                                            \
   (void)h3; (void)dout; (void)lout; (void)act; (void)rew; (void)hval; (void)nz_a; (void)nz_m;    \
   (void)flags; (void)alive; (void)s_nalive; (void)red; (void)v_nm; (void)v_ns; (void)v_lo; (void)v_hi;
   const int tile = blockIdx.x;
@@ -533,6 +544,21 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     if (w == 1 && j < S) v_ns[j] = p.norm_std[j] + 1e-6f;
     if (w == 2 && j < S1) v_lo[j] = p.min_lv[j];
     if (w == 3 && j < S1) v_hi[j] = p.max_lv[j];
+  }
+  if constexpr (LW) {
+    // packed mirrors: aW1 is [16 cb][1 k-step][256], aW3 [1 cb][16 k-steps][256];
+    // aW2 keeps k-steps [0, PERSIST_L2_LDS) of each of its 16 column blocks
+    const f32x4* a1 = reinterpret_cast<const f32x4*>(p.aW1);
+    const f32x4* a3 = reinterpret_cast<const f32x4*>(p.aW3);
+    const f32x4* a2 = reinterpret_cast<const f32x4*>(p.aW2);
+    for (int e = tid; e < 16 * 64; e += NT) {
+      reinterpret_cast<f32x4*>(wl1)[e] = gload(a1 + e);
+      reinterpret_cast<f32x4*>(wl3)[e] = gload(a3 + e);
+    }
+    for (int e = tid; e < 16 * PERSIST_L2_LDS * 64; e += NT) {
+      const int cb = e / (PERSIST_L2_LDS * 64), r = e - cb * PERSIST_L2_LDS * 64;
+      reinterpret_cast<f32x4*>(wl2)[e] = gload(a2 + cb * 16 * 64 + r);
+    }
   }
 
   // ---- initial states (t = 0): chronological replay index -> physical row -----
@@ -580,10 +606,19 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     int* alive_cur = (t & 1) ? flags : alive;
     int* alive_nxt = (t & 1) ? alive : flags;
     // ---- actor MLP (src/policy.py:61-100) ------------------------------------
-    tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh);
-    lds_barrier();
-    if (t == 2) RSTAMP(2);
-    tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
+    if constexpr (LW) {
+      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 1, 1>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh,
+                                                   GSave{nullptr, nullptr, 0, 0}, wl1);
+      lds_barrier();
+      if (t == 2) RSTAMP(2);
+      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 16, PERSIST_L2_LDS>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh,
+                                                                 GSave{nullptr, nullptr, 0, 0}, wl2);
+    } else {
+      tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh);
+      lds_barrier();
+      if (t == 2) RSTAMP(2);
+      tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
+    }
     lds_barrier();
     if (t == 2) RSTAMP(3);
     // ---- actor head + squashed Gaussian sample + model input [normalize(s), a]:
@@ -597,7 +632,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         bmu = gload(ab3 + d);
         braw = gload(ab3 + A + d);
       }
-      tile_dense_narrow_partials<NW, RB>(h2, ldh, Ha, step_opaque(p.aW3), red);
+      tile_dense_narrow_partials<NW, RB, LW>(h2, ldh, Ha, step_opaque(p.aW3), red, wl3);
       if (tid < ROWS * A) {
         const int r = tid / A, d = tid - r * A;
         const float mu = narrow_sum<NW, RB>(red, r, d) + bmu;
@@ -916,13 +951,19 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 3 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 8 +
                                                            64 + 2) + 4 + (size_t)nw * (rpt / 16) * 256 + 256);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
+  // LDS-resident actor weights (see rollout_persist_kernel) when they fit
+  const size_t lw_bytes = sizeof(float) * (size_t)(32 + 16 * PERSIST_L2_LDS) * 256;
+  const bool lw = rpt == 16 && NW == 8 && S <= 16 && d->Ha == 256 && 2 * A <= 16 && lds_bytes + lw_bytes <= 160 * 1024 &&
+                  !getenv("DRPO_ROLLOUT_NO_LDS_WEIGHTS");
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
   if (rpt == 32)
-    rollout_persist_kernel<2, 8><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+    rollout_persist_kernel<2, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   else if (NW == 16)
-    rollout_persist_kernel<1, 16><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);
+    rollout_persist_kernel<1, 16, false><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);
+  else if (lw)
+    rollout_persist_kernel<1, 8, true><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
   else
-    rollout_persist_kernel<1, 8><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+    rollout_persist_kernel<1, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   DRPO_LAUNCH_CHECK("rollout_persist");
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[1], stream);
   rollout_scan_kernel<<<H, 256, 0, stream>>>(a.cnt, pos, n, a.ntiles);
