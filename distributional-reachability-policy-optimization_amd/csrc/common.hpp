@@ -568,11 +568,12 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
 // [0, NCB1) come from mirror P1 (N1 outputs -> out1), [NCB1, NCB1+NCB2) from P2
 // (N2 -> out2). One pass instead of two halves the layer's serial latency and
 // gives each wave more independent accumulators.
-template <int NW, int RB, int MAXC, int ACT, int NK>
+template <int NW, int RB, int MAXC, int ACT, int NK, int RING = 0>
 __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, int K, const float* __restrict__ P1,
                                                      const float* __restrict__ b1, int N1, float* out1,
                                                      const float* __restrict__ P2, const float* __restrict__ b2,
-                                                     int N2, float* out2, int ldo) {
+                                                     int N2, float* out2, int ldo, const GSave& gs1,
+                                                     const GSave& gs2) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, g = lane >> 4;
@@ -589,16 +590,19 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
     const int col = cbs[c] * 16 + l15;
     const float* bb = second ? b2 : b1;
     const int nn = second ? N2 : N1;
-    bvs[c] = (bb && col < nn) ? bb[col] : 0.f;
+    bvs[c] = (bb && col < nn) ? gload(bb + col) : 0.f;
   }
   f32x4 acc[RB][MAXC];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 bq[PF_D][MAXC];
+  // ring depth (RING = 0: PF_D); a 4-waves-per-SIMD kernel has 128 VGPRs, where 2 fits
+  // 4 blocks per wave (one k-step ahead still covers 16 MFMAs per wave)
+  constexpr int PFP = RING > 0 ? RING : PF_D;
+  f32x4 bq[PFP][MAXC];
 #pragma unroll
-  for (int u = 0; u < PF_D - 1; ++u)
+  for (int u = 0; u < PFP - 1; ++u)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(Pc[c], cbs[c], min(u, NK - 1), NK);
   f32x4 an[RB], ac[RB];
@@ -606,9 +610,9 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
   for (int rb = 0; rb < RB; ++rb) an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
 #pragma unroll
   for (int s = 0; s < NK; ++s) {
-    if (s + PF_D - 1 < NK) {
+    if (s + PFP - 1 < NK) {
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c) bq[(s + PF_D - 1) % PF_D][c] = load_pk(Pc[c], cbs[c], s + PF_D - 1, NK);
+      for (int c = 0; c < MAXC; ++c) bq[(s + PFP - 1) % PFP][c] = load_pk(Pc[c], cbs[c], s + PFP - 1, NK);
     }
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
@@ -624,7 +628,7 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
       for (int c = 0; c < MAXC; ++c)
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
-          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF_D][c][m], acc[rb][c], 0, 0, 0);
+          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PFP][c][m], acc[rb][c], 0, 0, 0);
   }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
@@ -633,35 +637,45 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
     const bool second = cb >= NCB1;
     float* out = second ? out2 : out1;
     const int nn = second ? N2 : N1;
+    const GSave& gs = second ? gs2 : gs1;
     const int col = cbs[c] * 16 + l15;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rb * 16 + 4 * g + r;
-        out[row * ldo + col] = (col < nn) ? act_fn<ACT>(acc[rb][c][r] + bvs[c]) : 0.f;
+        const float z = acc[rb][c][r] + bvs[c];
+        const float y = act_fn<ACT>(z);
+        out[row * ldo + col] = (col < nn) ? y : 0.f;
+        if (col < nn && row < gs.nrows) {
+          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+        }
       }
   }
 }
 
-template <int NW, int RB, int NC, int ACT, int NK>
+template <int NW, int RB, int NC, int ACT, int NK, int RING = 0>
 __device__ __forceinline__ void tile_dense_pair_nc(int nc, const float* in, int ldi, int K, const float* P1,
                                                    const float* b1, int N1, float* out1, const float* P2,
-                                                   const float* b2, int N2, float* out2, int ldo) {
-  if (nc == NC) tile_dense_pair_core<NW, RB, NC, ACT, NK>(in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
+                                                   const float* b2, int N2, float* out2, int ldo, const GSave& gs1,
+                                                   const GSave& gs2) {
+  if (nc == NC) tile_dense_pair_core<NW, RB, NC, ACT, NK, RING>(in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1, gs2);
   else if constexpr (NC > 1)
-    tile_dense_pair_nc<NW, RB, NC - 1, ACT, NK>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
+    tile_dense_pair_nc<NW, RB, NC - 1, ACT, NK, RING>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1, gs2);
 }
 
 // per-wave block count dispatch as in tile_dense_impl
-template <int NW, int RB, int MAXC, int ACT, int NK>
+template <int NW, int RB, int MAXC, int ACT, int NK, int RING = 0>
 __device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K, const float* P1, const float* b1,
                                                 int N1, float* out1, const float* P2, const float* b2, int N2,
-                                                float* out2, int ldo) {
+                                                float* out2, int ldo,
+                                                const GSave& gs1 = GSave{nullptr, nullptr, 0, 0},
+                                                const GSave& gs2 = GSave{nullptr, nullptr, 0, 0}) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NCB = ((N1 + 15) >> 4) + ((N2 + 15) >> 4);
   const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
-  tile_dense_pair_nc<NW, RB, MAXC, ACT, NK>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo);
+  tile_dense_pair_nc<NW, RB, MAXC, ACT, NK, RING>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1, gs2);
 }
 
 // Partials-only form of tile_dense_narrow_pair (below): the value of layer `which`
@@ -727,7 +741,8 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
                                                        const float* __restrict__ P1, const float* __restrict__ b1,
                                                        int N1, float* out1, const float* __restrict__ P2,
                                                        const float* __restrict__ b2, int N2, float* out2, int ldo,
-                                                       float* red) {
+                                                       float* red, const GSave& gs1 = GSave{nullptr, nullptr, 0, 0},
+                                                       const GSave& gs2 = GSave{nullptr, nullptr, 0, 0}) {
   constexpr int HW = NW / 2;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -740,8 +755,8 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
   f32x4 acc[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float bias1 = (b1 && (tid & 15) < N1) ? b1[tid & 15] : 0.f;
-  const float bias2 = (b2 && (tid & 15) < N2) ? b2[tid & 15] : 0.f;
+  const float bias1 = (b1 && (tid & 15) < N1) ? gload(b1 + (tid & 15)) : 0.f;
+  const float bias2 = (b2 && (tid & 15) < N2) ? gload(b2 + (tid & 15)) : 0.f;
   constexpr int MAXS = (16 + HW - 1) / HW;      // K <= 256
   f32x4 b[MAXS], a[MAXS][RB];
 #pragma unroll
@@ -776,7 +791,14 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
     const int nn = which ? N2 : N1;
     const float z = v + (which ? bias2 : bias1);
     float* out = which ? out2 : out1;
-    out[(rb * 16 + rr) * ldo + col] = (col < nn) ? act_fn<ACT>(z) : 0.f;
+    const float y = act_fn<ACT>(z);
+    const int row = rb * 16 + rr;
+    out[row * ldo + col] = (col < nn) ? y : 0.f;
+    const GSave& gs = which ? gs2 : gs1;
+    if (col < nn && row < gs.nrows) {
+      if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+      if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+    }
   }
 }
 

@@ -13,6 +13,8 @@
 //  mlp_wgrad_kernel grouped dW = dZ^T Y (+ bias via a ones column) over all layers
 //                   of a parameter group in one launch, 64x64 output tiles x row
 //                   chunks, fp32 MFMA, atomically accumulated into the flat grad.
+#include <stdlib.h>
+
 #include "common.hpp"
 
 using namespace drpo;
@@ -201,6 +203,65 @@ __device__ __forceinline__ float* run_net_g(const drpo_mlp_fwd_t* __restrict__ a
   return cur;
 }
 
+// Trunk-mode job whose two heads are [256 -> N, act0] -> [N -> n<=16, act1] each (the
+// constraint critic's mean and log-std heads, src/ssac.py:46-92): both heads' hidden
+// layers run as ONE paired layer over the trunk output (2N output columns, one
+// k-loop) and both output layers as one split-K narrow pair, so the job's serial
+// chain is 4 layers instead of 6.
+__device__ __forceinline__ bool heads_pairable(const drpo_mlp_fwd_t* __restrict__ a) {
+  if (a->nnets != 3) return false;
+  const drpo_mlp_net_t& n1 = a->net[1];
+  const drpo_mlp_net_t& n2 = a->net[2];
+  return n1.nl == 2 && n2.nl == 2 && n1.L[0].din == 256 && n2.L[0].din == 256 && n1.L[0].dout == n2.L[0].dout &&
+         n1.L[0].act == n2.L[0].act && n1.L[1].act == n2.L[1].act && n1.L[1].dout <= 16 && n2.L[1].dout <= 16;
+}
+
+__device__ __forceinline__ GSave layer_save(const drpo_mlp_layer_t& L, int z, int64_t rows, int row0, int nrows) {
+  const size_t so = ((size_t)z * rows + row0) * L.dout;
+  return GSave{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
+}
+
+template <int RB, int ACT0, int ACT1>
+__device__ __forceinline__ void heads_pair_act(const drpo_mlp_fwd_t* __restrict__ a, const float* T, float* hA,
+                                               float* hB, float* o, int z, int row0, int nrows, float* red) {
+  const drpo_mlp_layer_t& A0 = a->net[1].L[0];
+  const drpo_mlp_layer_t& B0 = a->net[2].L[0];
+  const drpo_mlp_layer_t& A1 = a->net[1].L[1];
+  const drpo_mlp_layer_t& B1 = a->net[2].L[1];
+  tile_dense_pair<FW_NW, RB, 4, ACT0, 16, 2>(T, LDH, 256, A0.W + (size_t)z * A0.wstride, A0.b + (size_t)z * A0.bstride,
+                                          A0.dout, hA, B0.W + (size_t)z * B0.wstride, B0.b + (size_t)z * B0.bstride,
+                                          B0.dout, hB, LDH, layer_save(A0, z, a->rows, row0, nrows),
+                                          layer_save(B0, z, a->rows, row0, nrows));
+  lds_barrier();
+  tile_dense_narrow_pair<FW_NW, RB, ACT1>(hA, hB, LDH, A0.dout, A1.W + (size_t)z * A1.wstride,
+                                          A1.b + (size_t)z * A1.bstride, A1.dout, o, B1.W + (size_t)z * B1.wstride,
+                                          B1.b + (size_t)z * B1.bstride, B1.dout, o + 16, LDH, red,
+                                          layer_save(A1, z, a->rows, row0, nrows),
+                                          layer_save(B1, z, a->rows, row0, nrows));
+}
+
+template <int RB, int ACT0>
+__device__ __forceinline__ void heads_pair_act0(const drpo_mlp_fwd_t* __restrict__ a, const float* T, float* hA,
+                                                float* hB, float* o, int z, int row0, int nrows, float* red) {
+  switch (a->net[1].L[1].act) {
+    case ACT_RELU: heads_pair_act<RB, ACT0, ACT_RELU>(a, T, hA, hB, o, z, row0, nrows, red); break;
+    case ACT_SILU: heads_pair_act<RB, ACT0, ACT_SILU>(a, T, hA, hB, o, z, row0, nrows, red); break;
+    case ACT_TANH: heads_pair_act<RB, ACT0, ACT_TANH>(a, T, hA, hB, o, z, row0, nrows, red); break;
+    default: heads_pair_act<RB, ACT0, ACT_NONE>(a, T, hA, hB, o, z, row0, nrows, red); break;
+  }
+}
+
+template <int RB>
+__device__ __forceinline__ void heads_pair(const drpo_mlp_fwd_t* __restrict__ a, const float* T, float* hA, float* hB,
+                                           float* o, int z, int row0, int nrows, float* red) {
+  switch (a->net[1].L[0].act) {
+    case ACT_RELU: heads_pair_act0<RB, ACT_RELU>(a, T, hA, hB, o, z, row0, nrows, red); break;
+    case ACT_SILU: heads_pair_act0<RB, ACT_SILU>(a, T, hA, hB, o, z, row0, nrows, red); break;
+    case ACT_TANH: heads_pair_act0<RB, ACT_TANH>(a, T, hA, hB, o, z, row0, nrows, red); break;
+    default: heads_pair_act0<RB, ACT_NONE>(a, T, hA, hB, o, z, row0, nrows, red); break;
+  }
+}
+
 template <int RB>
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ? 4 : 2, RB == 1 ? 4 : 2))) void mlp_fwd_multi_kernel(MultiArgs m) {
   constexpr int ROWS = 16 * RB;
@@ -237,6 +298,12 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   float* outp;
   if (!a->trunk) {
     outp = run_net_g<RB>(a, net, xin, bA, bB, z, row0, nrows, red);
+  } else if (heads_pairable(a)) {
+    // trunk output stays where the trunk left it; the paired heads use the two
+    // other full buffers and write their narrow outputs into xin (consumed)
+    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
+    outp = nullptr;
+    heads_pair<RB>(a, t, T, t == bA ? bB : bA, xin, z, row0, nrows, red);
   } else {
     float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
     const int w = a->net[0].L[a->net[0].nl - 1].dout;
@@ -301,7 +368,11 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
   // 32-row tiles halve the weight bytes per MFMA but allow only one 8-wave workgroup
   // per CU (LDS); measured slower at B=4096 (profiles/r01), so only for launches
   // with >= 8 workgroups per CU at 16-row tiles
-  if (tiles * slots * nbatch >= 2048) {
+  static const int force_rb = [] {
+    const char* e = getenv("DRPO_FWD_RB");
+    return e ? atoi(e) : 0;
+  }();
+  if (force_rb == 2 || (force_rb != 1 && tiles * slots * nbatch >= 2048)) {
     const size_t lds = sizeof(float) * ((size_t)4 * 2 * FW_ROWS * LDH + FW_NW * 2 * 256);
     mlp_fwd_multi_kernel<2><<<dim3((unsigned)((tiles + 1) / 2), slots, nbatch), FW_NT, lds, stream>>>(m);
   } else {
