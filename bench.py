@@ -1,17 +1,27 @@
 #!/usr/bin/env python
 """Hot-path benchmark: imagined transitions/s + SAC grad-steps/s (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): quadrotor (S=12, A=2, C=2), ensemble E=7,
-horizon H=10, batch B=4096 (rollout_batch_size = sac batch_size = B), DRPO flags
-(qc_under_uncertainty = distributional_qc = mlp_multiplier = True), reference
-default widths (actor/critics 256, model 200). Synthetic replay of 100k rows per
-SURVEY.md §8(d); random-init weights in "steady" rollout mode (diff-head output
-layer zeroed, log-var output bias -20) so every rollout writes exactly B*H rows.
+Workloads (BASELINE.json configs, restated as concrete inputs in SURVEY.md §8(d)),
+picked with --config (default 2, the configuration the metric is quoted on):
+
+  1  cartpole-move  (S=4,  A=1, C=4)  E=3  H=5   B=256
+  2  quadrotor      (S=12, A=2, C=2)  E=7  H=10  B=4096
+  3  point-robot    (S=11, A=2, C=1)  E=7  H=20  B=8192
+  4  tracking       (S=51, A=2, C=1)  E=8  H=40  B=16384   (ensemble-sharded fit under torchrun)
+  5  quadrotor      (S=12, A=2, C=2)  E=32 H=80  B=65536   (global batch: B/N rows per rank)
+
+"batch" is both rollout_batch_size and the SAC batch size. DRPO flags
+(qc_under_uncertainty = distributional_qc = mlp_multiplier = True), the other
+hyper-parameters from the env's reference JSON (config/*.json), reference default
+widths (actor/critics 256, model 200). Synthetic replay of 100k rows per §8(d);
+random-init weights in "steady" rollout mode (diff-head output layer zeroed,
+log-var output bias -20) so every rollout writes exactly B*H rows.
 
 One step = SMBPO.rollout_and_update(): 1 rollout of B*H imagined transitions +
-10 update_solver calls (actor on every 2nd, multiplier on every 5th). With
---gpus N (torchrun), each rank runs its own rollout shard of B rows and its own
-SAC minibatch of B rows with gradients all-reduced over RCCL (weak scaling).
+10 update_solver calls (actor on every 2nd, multiplier on every 5th). Under
+torchrun every rank rolls out its own B rows and draws its own SAC minibatch of B
+rows with gradients all-reduced over RCCL (weak scaling); config 5 divides its
+global batch over the ranks instead (strong scaling).
 
 value = imagined transitions/s over the rollout phases of the timed region (all
 ranks); sac.value = SAC grad-steps/s over the update phases. ms_per_step is the
@@ -31,6 +41,51 @@ sys.path.insert(0, ROOT)
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (matrix == vector rate), /opt/skills/guides/MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+METRIC = 'imagined transitions/sec + SAC grad-steps/sec, quadrotor @1/2/4/8 GPU'
+
+ENV_DIMS = {'cartpole': (4, 1, 4), 'quadrotor': (12, 2, 2), 'point-robot': (11, 2, 1), 'tracking': (51, 2, 1)}
+
+# reference config/*.json alg_cfg (the DRPO flags are set by make_alg, as run.sh does)
+ENV_JSON = {
+    'quadrotor': {
+        'sac_cfg': {'target_entropy': -2.0, 'constraint_threshold': 0.0, 'mlp_multiplier': True, 'penalty_lb': -1.0,
+                    'penalty_ub': 100.0, 'mlp_multiplier_cfg': {'upper_bound': 50.0},
+                    'constraint_critic_cfg': {'std_ratio': 2.0}, 'actor_lr': 1e-4, 'actor_lr_end': 4e-5},
+        'steps_per_epoch': 360, 'model_update_period': 90, 'model_initial_steps': 1000, 'model_steps': 1000,
+        'buffer_min': 1800, 'reward_scale': 2.0, 'alive_bonus': 2.0, 'safe_shield': False,
+        'safe_shield_threshold': -0.2, 'eval_shield_threshold': -0.1, 'constraint_offset': 0.5},
+    'point-robot': {
+        'sac_cfg': {'target_entropy': -2.0, 'constraint_threshold': 0.0, 'penalty_lb': -5.0, 'penalty_ub': 100.0,
+                    'mlp_multiplier_cfg': {'upper_bound': 50.0}, 'constraint_critic_cfg': {'std_ratio': 2.0},
+                    'actor_lr': 1e-4, 'actor_lr_end': 4e-5},
+        'steps_per_epoch': 300, 'model_update_period': 75, 'model_initial_steps': 5000, 'model_steps': 1000,
+        'buffer_min': 1500, 'reward_scale': 10.0, 'alive_bonus': 0.0, 'constraint_scale': 10.0,
+        'safe_shield': False},
+    'tracking': {
+        'sac_cfg': {'target_entropy': -2.0, 'constraint_threshold': 0.0, 'penalty_lb': -5.0, 'penalty_ub': 100.0,
+                    'mlp_multiplier_cfg': {'upper_bound': 50.0}, 'constraint_critic_cfg': {'std_ratio': 1.0},
+                    'actor_lr': 5e-5, 'actor_lr_end': 1e-7},
+        'steps_per_epoch': 200, 'model_update_period': 50, 'model_initial_steps': 2000, 'model_steps': 1000,
+        'buffer_min': 1000, 'reward_scale': 20.0, 'alive_bonus': 2.0, 'constraint_scale': 5.0, 'safe_shield': False,
+        'real_fraction': 1.0},
+    'cartpole': {
+        'sac_cfg': {'target_entropy': -1.0, 'constraint_threshold': 0.0, 'penalty_lb': -5.0, 'penalty_ub': 100.0,
+                    'mlp_multiplier_cfg': {'upper_bound': 50.0}, 'constraint_critic_cfg': {'std_ratio': 2.0},
+                    'actor_lr': 1e-4, 'actor_lr_end': 4e-5},
+        'steps_per_epoch': 1000, 'model_update_period': 250, 'model_initial_steps': 2000, 'model_steps': 1000,
+        'buffer_min': 1000, 'reward_scale': 1.0, 'alive_bonus': 0.0, 'constraint_scale': 100.0, 'safe_shield': False},
+}
+QUAD_JSON = ENV_JSON['quadrotor']
+
+CONFIGS = {
+    1: dict(env='cartpole', E=3, H=5, B=256, label='cartpole-move E=3 H=5 B=256 (BASELINE configs[0])'),
+    2: dict(env='quadrotor', E=7, H=10, B=4096, label='quadrotor E=7 H=10 B=4096 (BASELINE configs[1])'),
+    3: dict(env='point-robot', E=7, H=20, B=8192, label='point-robot E=7 H=20 B=8192 (BASELINE configs[2])'),
+    4: dict(env='tracking', E=8, H=40, B=16384,
+            label='tracking-double_lane E=8 H=40 B=16384, ensemble-sharded fit (BASELINE configs[3])'),
+    5: dict(env='quadrotor', E=32, H=80, B=65536, global_batch=True,
+            label='quadrotor E=32 H=80 global B=65536, DP all-reduce (BASELINE configs[4])'),
+}
 
 
 def rollout_flop_per_transition(S, A, Ha=256, Hm=200):
@@ -59,19 +114,82 @@ def fit_flop_per_step(S, A, E, b, Hm=200):
     return 3 * 2 * mac * E * b
 
 
-def synth_replay(S, A, C, N, rng):
-    s = rng.normal(0, 0.1, size=(N, S)).astype(np.float32)
-    s[:, 0] = rng.uniform(-1, 1, N)
-    s[:, 2] = rng.uniform(0.8, 1.2, N)
-    s[:, 4] = rng.uniform(-0.1, 0.1, N)
+# ---------------------------------------------------------------------------
+# synthetic replays
+# ---------------------------------------------------------------------------
+def _point_robot_obs(xy, v, th):
+    """11-d point-robot observation from (x, y, v, heading) (src/env/point_robot.py:146-170)."""
+    n = len(v)
+    o = np.zeros((n, 11), np.float32)
+    o[:, 0:2], o[:, 2] = xy, v
+    c, s = np.cos(th), np.sin(th)
+    o[:, 3], o[:, 4] = c, s
+    for i, hz in enumerate(((0.4, -1.2), (-0.4, 1.2))):
+        dx, dy = hz[0] - xy[:, 0], hz[1] - xy[:, 1]
+        bx, by = dx * c + dy * s, -dx * s + dy * c      # (hazard - pos) @ [[c, -s], [s, c]]
+        o[:, 5 + 3 * i] = np.hypot(bx, by)
+        ang = np.arctan2(by, bx)
+        o[:, 6 + 3 * i], o[:, 7 + 3 * i] = np.cos(ang), np.sin(ang)
+    return o
+
+
+def synth_states(env, N, rng):
+    if env == 'quadrotor':
+        s = rng.normal(0, 0.1, size=(N, 12)).astype(np.float32)
+        s[:, 0] = rng.uniform(-1, 1, N)
+        s[:, 2] = rng.uniform(0.8, 1.2, N)
+        s[:, 4] = rng.uniform(-0.1, 0.1, N)
+        return s
+    if env == 'cartpole':
+        s = rng.normal(0, 0.1, size=(N, 4)).astype(np.float32)
+        s[:, 0] = rng.uniform(-0.5, 0.5, N)
+        s[:, 1] = rng.uniform(-0.1, 0.1, N)
+        return s
+    if env == 'point-robot':
+        xy = rng.uniform(-2.5, 2.5, size=(N, 2))
+        near = rng.rand(N) < 0.25       # ~25 % of rows within 0.3 of a hazard's edge
+        hz = np.array([[0.4, -1.2], [-0.4, 1.2]])[rng.randint(0, 2, N)]
+        ang = rng.uniform(0, 2 * np.pi, N)
+        rad = 0.8 + rng.uniform(-0.3, 0.3, N)
+        xy[near] = hz[near] + rad[near, None] * np.stack([np.cos(ang[near]), np.sin(ang[near])], 1)
+        goal = np.hypot(xy[:, 0] - 2.2, xy[:, 1] - 2.2) <= 0.3
+        xy[goal] = -xy[goal]            # reject the goal disc
+        return _point_robot_obs(xy, rng.uniform(0.5, 2.0, N), rng.uniform(np.pi / 4, 3 * np.pi / 4, N))
+    if env == 'tracking':
+        s = rng.normal(0, 0.5, size=(N, 51)).astype(np.float32)
+        hi = np.array([2, 1, np.pi / 6, 2, 0.1, 0.1])       # work_space (pyth_veh3dofconti_data.py:87-91)
+        s[:, 0:6] = rng.uniform(-hi, hi, size=(N, 6))
+        s[:, 6] = rng.uniform(-np.pi / 6, np.pi / 6, N)
+        lon, lat = rng.uniform(-15, 15, N), rng.uniform(-5, 5, N)
+        clash = (np.abs(lon) <= 7) & (np.abs(lat) <= 3)
+        lon[clash] = np.sign(lon[clash]) * (7 + rng.uniform(0.01, 8, clash.sum()))
+        s[:, 47], s[:, 48] = lon, lat
+        s[:, 49], s[:, 50] = rng.normal(0, 0.1, N), rng.uniform(5, 10, N)
+        return s
+    raise KeyError(env)
+
+
+def synth_replay(env, N, rng, dev=None, env_params=None):
+    """states, actions, next states (s + N(0, 1e-3)), rewards ~ N(0, 1) and the env's
+    constraint values / flags of the next states (device constraint fns when dev is a
+    GPU, else zeros)."""
+    S, A, C = ENV_DIMS[env]
+    s = synth_states(env, N, rng)
     a = rng.uniform(-1, 1, size=(N, A)).astype(np.float32)
     s2 = (s + rng.normal(0, 1e-3, size=s.shape)).astype(np.float32)
-    h = np.stack([0.5 - s2[:, 2], s2[:, 2] - 1.5], 1).astype(np.float32)
-    return dict(states=s, actions=a, next_states=s2, rewards=rng.normal(0, 1, N).astype(np.float32),
-                dones=np.zeros(N, bool), violations=np.zeros(N, bool), constraint_values=h)
+    rep = dict(states=s, actions=a, next_states=s2, rewards=rng.normal(0, 1, N).astype(np.float32),
+               dones=np.zeros(N, bool), violations=np.zeros(N, bool),
+               constraint_values=np.zeros((N, C) if C > 1 else N, np.float32))
+    if dev is not None and dev.type == 'cuda':
+        from drpo_amd import ops
+        from drpo_amd.envs import device_env_params
+        d, v, h = ops.env_constraints(env_params or device_env_params(env), torch.from_numpy(s2).to(dev))
+        rep['dones'], rep['violations'], rep['constraint_values'] = (d.cpu().numpy(), v.cpu().numpy(),
+                                                                      h.cpu().numpy())
+    return rep
 
 
-def make_alg(dev, B, H, E, seed, cfg_json, extra=None):
+def make_alg(dev, B, H, E, seed, cfg_json, extra=None, env='quadrotor'):
     import drpo_amd
     from drpo_amd.envs import ShapeEnv
     cfg = drpo_amd.SMBPO.Config()
@@ -83,17 +201,7 @@ def make_alg(dev, B, H, E, seed, cfg_json, extra=None):
     if extra:
         cfg.update(extra)
     drpo_amd.set_seed(seed)
-    alg = drpo_amd.SMBPO(cfg, lambda id=None: ShapeEnv('quadrotor'), None, 100, device=dev, noise_seed=seed)
-    return alg
-
-
-QUAD_JSON = {  # reference config/quadrotor.json alg_cfg (DRPO flags set by make_alg, as run.sh does)
-    'sac_cfg': {'target_entropy': -2.0, 'constraint_threshold': 0.0, 'mlp_multiplier': True, 'penalty_lb': -1.0,
-                'penalty_ub': 100.0, 'mlp_multiplier_cfg': {'upper_bound': 50.0},
-                'constraint_critic_cfg': {'std_ratio': 2.0}, 'actor_lr': 1e-4, 'actor_lr_end': 4e-5},
-    'steps_per_epoch': 360, 'model_update_period': 90, 'model_initial_steps': 1000, 'model_steps': 1000,
-    'buffer_min': 1800, 'reward_scale': 2.0, 'alive_bonus': 2.0, 'safe_shield': False,
-    'safe_shield_threshold': -0.2, 'eval_shield_threshold': -0.1, 'constraint_offset': 0.5}
+    return drpo_amd.SMBPO(cfg, lambda id=None: ShapeEnv(env), None, 100, device=dev, noise_seed=seed)
 
 
 def steady_mode(alg):
@@ -105,58 +213,84 @@ def steady_mode(alg):
     m._elite_inds = list(range(min(5, m.ensemble_size)))
 
 
-def cpu_baseline(B, H, E, seed, budget_s=12.0):
-    """Oracle (torch-CPU restatement of the reference) on the host: one bounded sample."""
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline(cfgd, seed, budget_s=16.0):
+    """The oracle (torch-CPU restatement of the reference, pinned to its fixtures) on
+    the host: a bounded sample of the same workload at 4 threads (the reference's
+    torch.set_num_threads(4), src/cli.py:108) and at every core this process may use."""
     from oracle import drpo_oracle as O
-    threads = 4                         # the reference's torch.set_num_threads(4) (src/cli.py:108)
-    torch.set_num_threads(threads)
+    env, E = cfgd['env'], cfgd['E']
+    S, A, C = ENV_DIMS[env]
+    jsn = ENV_JSON[env]
+    Bs, Hs = min(cfgd['B'], 4096), min(cfgd['H'], 10)      # bounded sample of the workload
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    share = int(os.environ.get('OMP_NUM_THREADS', affinity))
+    all_threads = max(1, min(affinity, share))
     dev = torch.device('cpu')
-    import drpo_amd  # noqa: F401  (init replication only; no compute on CPU)
-    alg = make_alg(dev, B, H, E, seed, QUAD_JSON)
+    alg = make_alg(dev, Bs, Hs, E, seed, jsn, env=env)
     steady_mode(alg)
     sd = {k: v.detach().clone() for k, v in alg.state_dict().items()}
-    rng = np.random.RandomState(seed)
-    rep = synth_replay(12, 2, 2, 100000, rng)
+    rep = synth_replay(env, 100000, np.random.RandomState(seed))
     st = torch.from_numpy(rep['states'])
     P = {k[len('solver.'):]: v for k, v in sd.items() if k.startswith('solver.actor.')}
     P.update({k: v for k, v in sd.items() if k.startswith('model_ensemble.')})
     P['model_ensemble.state_normalizer.mean'], P['model_ensemble.state_normalizer.std'] = O.normalizer_fit(st)
     elites = list(range(min(5, E)))
-    n_tr, t0 = 0, time.perf_counter()
-    reps = 0
-    while time.perf_counter() - t0 < budget_s / 2 or reps < 1:
-        out = O.rollout(P, 'actor.net.', 'model_ensemble.', elites, st, 'quadrotor', B, H, O.LiveRNG())
-        n_tr += len(out['states'])
-        reps += 1
-    roll_tps = n_tr / (time.perf_counter() - t0)
-    # SAC: oracle update_critic / update_actor_and_alpha / update_multiplier at the
-    # rollout_and_update cadence on batches drawn from the same synthetic replay
     Ps = {k[len('solver.'):]: v for k, v in sd.items() if k.startswith('solver.') and
           not k.startswith('solver.model_ensemble') and k != 'solver.total_updates'}
-    orc = O.SSACOracle(Ps, dict(batch_size=B, target_entropy=-2.0, penalty_lb=-1.0, actor_lr=1e-4,
-                                updates_per_training=100 * 360 * 10), 2, 2)
-    live = O.LiveRNG()
+    sac_cfg = jsn['sac_cfg']
     r = torch.from_numpy(rep['rewards'])
-    hcv = torch.from_numpy(rep['constraint_values'])
-    t1, steps = time.perf_counter(), 0
-    while time.perf_counter() - t1 < budget_s / 2 or steps < 2:
-        idx = torch.randint(len(st), [B])
-        batch = (st[idx], torch.from_numpy(rep['actions'])[idx], torch.from_numpy(rep['next_states'])[idx],
-                 r[idx] * 2.0 + 2.0, torch.zeros(B, dtype=torch.bool), torch.zeros(B, dtype=torch.bool),
-                 hcv[idx] * 10.0 + (hcv[idx] > 0).float() * 0.5)
-        orc.update_critic(*batch, live)
-        if steps % 2 == 0:
-            orc.update_actor_and_alpha(batch[0], live)
-        if steps % 5 == 0:
-            orc.update_multiplier(batch[0], live)
-        steps += 1
-    sac_sps = steps / (time.perf_counter() - t1)
-    return {'value': roll_tps, 'unit': 'imagined transitions/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{reps} x oracle SMBPO.rollout (quadrotor B={B} H={H} E={E}, steady mode) on the host CPU '
-                      f'(torch {torch.__version__}, {threads} threads)',
-            'sac': {'value': sac_sps, 'unit': f'grad-steps/s of B={B} samples',
-                    'sample': f'{steps} x oracle update_solver cadence (critic; actor 1/2; multiplier 1/5), '
-                              f'B={B}, {threads} threads'}}
+    hcv = torch.from_numpy(rep['constraint_values']).reshape(len(r), -1)
+    out = {}
+    for threads in sorted({4, all_threads}):
+        torch.set_num_threads(threads)
+        n_tr, reps, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s / 4 or reps < 1:
+            ro = O.rollout(P, 'actor.net.', 'model_ensemble.', elites, st, env, Bs, Hs, O.LiveRNG())
+            n_tr += len(ro['states'])
+            reps += 1
+        roll = n_tr / (time.perf_counter() - t0)
+        orc = O.SSACOracle(Ps, dict(batch_size=Bs, target_entropy=sac_cfg['target_entropy'],
+                                    penalty_lb=sac_cfg['penalty_lb'], actor_lr=sac_cfg['actor_lr'],
+                                    updates_per_training=100 * jsn['steps_per_epoch'] * 10), C, A)
+        live = O.LiveRNG()
+        t1, steps = time.perf_counter(), 0
+        while time.perf_counter() - t1 < budget_s / 4 or steps < 2:
+            idx = torch.randint(len(st), [Bs])
+            h = hcv[idx] * jsn.get('constraint_scale', 10.0)
+            h = h + (h > 0).float() * jsn.get('constraint_offset', 0.0)
+            batch = (st[idx], torch.from_numpy(rep['actions'])[idx], torch.from_numpy(rep['next_states'])[idx],
+                     r[idx] * jsn['reward_scale'] + jsn['alive_bonus'], torch.zeros(Bs, dtype=torch.bool),
+                     torch.zeros(Bs, dtype=torch.bool), h if C > 1 else h[:, 0])
+            orc.update_critic(*batch, live)
+            if steps % 2 == 0:
+                orc.update_actor_and_alpha(batch[0], live)
+            if steps % 5 == 0:
+                orc.update_multiplier(batch[0], live)
+            steps += 1
+        sps = steps / (time.perf_counter() - t1)
+        out[threads] = (roll, reps, sps, steps)
+    t4 = out[4]
+    ta = out[all_threads]
+    return {'value': t4[0], 'unit': 'imagined transitions/s', 'cores': 4, 'kind': 'port',
+            'sample': f'{t4[1]} x oracle SMBPO.rollout of B={Bs} H={Hs} ({env}, E={E}, steady mode) on the host CPU, '
+                      f'torch {torch.__version__}, 4 threads (bounded sample of the B={cfgd["B"]} H={cfgd["H"]} '
+                      'workload)',
+            'cpu_model': cpu_model(), 'cores_available': affinity, 'cpu_share_threads': share,
+            'all_cores': {'threads': all_threads, 'value': ta[0],
+                          'sac_value': ta[2], 'sac_samples_per_s': ta[2] * Bs},
+            'sac': {'value': t4[2], 'unit': f'grad-steps/s of B={Bs} samples', 'samples_per_s': t4[2] * Bs,
+                    'sample': f'{t4[3]} x oracle update_solver cadence (critic; actor 1/2; multiplier 1/5), '
+                              f'B={Bs}, 4 threads'}}
 
 
 def main():
@@ -164,9 +298,13 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=4096)
-    ap.add_argument('--horizon', type=int, default=10)
-    ap.add_argument('--ensemble', type=int, default=7)
+    ap.add_argument('--config', type=int, default=2, choices=sorted(CONFIGS),
+                    help='BASELINE.json configs[config-1] (SURVEY.md §8(d))')
+    ap.add_argument('--batch', type=int, default=None, help='override B (per rank; labels the run as custom)')
+    ap.add_argument('--horizon', type=int, default=None)
+    ap.add_argument('--ensemble', type=int, default=None)
+    ap.add_argument('--global-batch', type=int, default=None,
+                    help='divide this global batch over the ranks (config 5 does so by default)')
     ap.add_argument('--rollout-only', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--seed', type=int, default=0)
@@ -191,27 +329,34 @@ def main():
             dist.init_process_group(args.backend)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
-    B, H, E = args.batch, args.horizon, args.ensemble
 
-    import drpo_amd
+    cfgd = dict(CONFIGS[args.config])
+    env = cfgd['env']
+    S, A, C = ENV_DIMS[env]
+    E = args.ensemble or cfgd['E']
+    H = args.horizon or cfgd['H']
+    gb = args.global_batch or (cfgd['B'] if cfgd.get('global_batch') else None)
+    if gb is not None:
+        assert gb % world == 0, f'global batch {gb} must divide over {world} ranks'
+        B = gb // world
+    else:
+        B = args.batch or cfgd['B']
+    custom = any(x is not None for x in (args.batch, args.horizon, args.ensemble, args.global_batch))
+    label = cfgd['label'] if not custom else f'{env} E={E} H={H} B={B}/rank (custom shape, not a BASELINE config)'
+
+    import drpo_amd  # noqa: F401
     from drpo_amd.ops import EventTimer
-    alg = make_alg(dev, B, H, E, args.seed + rank, QUAD_JSON)
+    alg = make_alg(dev, B, H, E, args.seed, ENV_JSON[env], env=env)
     alg.rollout_engine = args.engine
-    rep = synth_replay(12, 2, 2, 100000, np.random.RandomState(args.seed + rank))
+    rep = synth_replay(env, 100000, np.random.RandomState(args.seed + rank), dev, alg.env_params)
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     steady_mode(alg)
     from drpo_amd.distributed import sync_parameters
     sync_parameters(alg)            # every rank starts from rank 0's weights (DP replicas)
     do_sac = not args.rollout_only
-    if do_sac:
-        try:
-            alg.solver.engine   # noqa: B018
-        except (ImportError, NotImplementedError):
-            do_sac = False
 
-    roll_ms, sac_ms, kern_ms, step_ms, n_trans = [], [], [], [], 0
-
+    roll_ms, sac_ms, kern_ms = [], [], []
     n_dev = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def one_step(tmr):
@@ -298,10 +443,11 @@ def main():
         fit_s = fit_s.item()
         from drpo_amd.distributed import member_sharding
         sh = member_sharding(m)
-        fl = fit_flop_per_step(12, 2, E, m.batch_size, m.hidden_dim)
+        fl = fit_flop_per_step(S, A, E, m.batch_size, m.hidden_dim)
         fit_res = {'steps': args.fit_steps, 'ms_per_fit_step': fit_s / args.fit_steps * 1e3,
                    'fit_steps_per_s': args.fit_steps / fit_s, 'flop_per_fit_step': fl,
                    'achieved_tflops_job': fl * args.fit_steps / fit_s / 1e12,
+                   'frac_job': fl * args.fit_steps / fit_s / 1e12 / (FP32_PEAK_TFLOPS * world),
                    'rows_per_step': E * m.batch_size,
                    'sharding': f'members {sh.ranges}' if sh is not None else
                    ('batch (gradient all-reduce)' if world > 1 else 'single')}
@@ -311,31 +457,32 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    flop_tr = rollout_flop_per_transition(12, 2)
+    flop_tr = rollout_flop_per_transition(S, A)
     fused = getattr(timers[0], 'pairs', H) == 1
     kname = 'rollout_persist_kernel' if fused else 'rollout_step_kernel'
     k_avg_ms = float(np.mean(kern_ms))
     rows_per_launch = n_trans / max(1, len(kern_ms))
     achieved = flop_tr * rows_per_launch / (k_avg_ms * 1e-3) / 1e12
+    sac_flop = sac_flop_per_step(B, S, A, C)
     res = {
-        'metric': 'imagined transitions/sec + SAC grad-steps/sec, quadrotor @1/2/4/8 GPU',
+        'metric': METRIC,
         'value': n_all / roll_s,
         'unit': 'imagined transitions/s',
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': wall / args.steps * 1e3,
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'fp32', 'data': 'synthetic (SURVEY.md §8(d) quadrotor replay, random-init weights, steady mode)',
-        'config': {'workload': 'quadrotor E=7 H=10 B=4096 (BASELINE configs[1])', 'env': 'quadrotor',
+        'higher_is_better': True, 'scaling': 'strong' if gb is not None else 'weak', 'vs_baseline': None,
+        'dtype': 'fp32', 'data': f'synthetic (SURVEY.md §8(d) {env} replay, random-init weights, steady mode)',
+        'config': {'workload': label, 'baseline_config': None if custom else args.config, 'env': env,
                    'ensemble': E, 'horizon': H, 'batch': B, 'global_batch': B * world,
                    'parallelism': f'dp{world}' if world > 1 else 'single', 'drpo_flags': True},
-        'sac': {'metric': 'SAC grad-steps/sec', 'unit': f'grad-steps/s of B={B} samples (whole job)',
-                'value': (alg.solver_updates_per_step * args.steps * world / sac_s) if do_sac and sac_s > 0 else None,
-                'global_steps_per_s': (alg.solver_updates_per_step * args.steps / sac_s)
-                if do_sac and sac_s > 0 else None,
+        'sac': {'metric': 'SAC grad-steps/sec', 'unit': f'grad-steps/s of B={B * world} samples (whole job)',
+                'value': (alg.solver_updates_per_step * args.steps / sac_s) if do_sac and sac_s > 0 else None,
+                'rank_steps_per_s': (alg.solver_updates_per_step * args.steps / sac_s) if do_sac and sac_s > 0
+                else None,
                 'global_batch': B * world, 'gradient_exchange': 'RCCL all-reduce (mean) per optimizer group'
                 if world > 1 else None,
-                'flop_per_step': sac_flop_per_step(B), 'measured': do_sac,
-                'achieved_tflops_per_gpu': (sac_flop_per_step(B) * alg.solver_updates_per_step * args.steps / sac_s / 1e12)
+                'flop_per_step_per_rank': sac_flop, 'measured': do_sac,
+                'achieved_tflops_per_gpu': (sac_flop * alg.solver_updates_per_step * args.steps / sac_s / 1e12)
                 if do_sac and sac_s > 0 else None,
                 'mlp_kernels': sac_kernels},
         'model_fit': fit_res,
@@ -344,13 +491,18 @@ def main():
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,
                      'rows_per_launch': rows_per_launch},
     }
-    prof = os.path.join(ROOT, 'profiles', 'traffic_rollout_fused.json' if fused else 'traffic_rollout_step.json')
-    if os.path.exists(prof):
-        tr = json.load(open(prof))
-        if tr.get('kernel') == kname:
-            res['roofline']['traffic'] = tr.get('bytes_per_launch')
+    if res['sac']['achieved_tflops_per_gpu'] is not None:
+        res['sac']['frac'] = res['sac']['achieved_tflops_per_gpu'] / FP32_PEAK_TFLOPS
+    base = 'traffic_rollout_fused' if fused else 'traffic_rollout_step'
+    for prof in (os.path.join(ROOT, 'profiles', f'{base}_c{args.config}.json'),
+                 os.path.join(ROOT, 'profiles', f'{base}.json') if args.config == 2 else None):
+        if prof and os.path.exists(prof) and not custom:
+            tr = json.load(open(prof))
+            if tr.get('kernel') == kname:
+                res['roofline']['traffic'] = tr.get('bytes_per_launch')
+                break
     if world == 1 and not args.no_cpu_baseline:
-        res['cpu_baseline'] = cpu_baseline(B, H, E, args.seed)
+        res['cpu_baseline'] = cpu_baseline(cfgd, args.seed)
     print(json.dumps(res))
     if dist is not None:
         dist.destroy_process_group()

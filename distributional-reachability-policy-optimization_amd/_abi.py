@@ -3,7 +3,7 @@ suite checks every declared symbol is exported and every prototype here exists i
 the header)."""
 import ctypes
 
-from ctypes import c_int, c_int64, c_uint64, c_float, c_size_t, c_void_p, c_char_p, POINTER
+from ctypes import c_int, c_int64, c_uint64, c_float, c_double, c_size_t, c_void_p, c_char_p, POINTER
 
 P = c_void_p
 
@@ -13,7 +13,7 @@ class RolloutDesc(ctypes.Structure):
     _fields_ = [
         ('S', c_int), ('A', c_int), ('C', c_int), ('Ha', c_int), ('Hm', c_int), ('B', c_int), ('H', c_int),
         ('env_id', c_int), ('tracking_surr_start', c_int), ('tracking_n_surr', c_int),
-        ('quad_x_threshold', c_float), ('quad_z_threshold', c_float),
+        ('env_thr0', c_double), ('env_thr1', c_double),
         ('aW1', P), ('ab1', P), ('aW2', P), ('ab2', P), ('aW3', P), ('ab3', P),
         ('mW1', P), ('mb1', P), ('mW2', P), ('mb2', P), ('dW1', P), ('db1', P), ('dW2', P), ('db2', P),
         ('lW1', P), ('lb1', P), ('lW2', P), ('lb2', P),
@@ -58,7 +58,9 @@ PROTOTYPES = {
     'drpo_rollout_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'drpo_rollout_count_offset': (c_size_t, [c_int, c_int, c_int]),
     'drpo_rollout': (c_int, [POINTER(RolloutDesc), P]),
-    'drpo_env_constraints': (c_int, [c_int, c_int, c_int, c_float, c_float, P, c_int64, c_int, P, P, P, P]),
+    'drpo_env_constraints': (c_int, [c_int, c_int, c_int, c_double, c_double, P, c_int64, c_int, P, P, P, P]),
+    'drpo_shield_mix': (c_int, [P, P, c_int64, c_int, c_int, P, P]),
+    'drpo_shield_select': (c_int, [P, c_int, c_int64, c_int, c_int, c_int, c_float, P, P, P, P, P]),
     'drpo_sample_without_replacement': (c_int, [P, c_int64, c_int64, c_uint64, c_uint64, P]),
     'drpo_event_create': (c_int, [POINTER(c_void_p)]),
     'drpo_event_destroy': (c_int, [P]),

@@ -14,7 +14,7 @@ struct EnvParams {
   int id;
   int surr_start;     // tracking: first surrounding-vehicle dim (47 for ref_num 1 / pre_horizon 10)
   int n_surr;         // tracking: number of surrounding vehicles
-  float quad_x_threshold, quad_z_threshold;   // safe_control_gym values (unpinned)
+  double thr0, thr1;  // quadrotor: x/z_threshold (safe_control_gym, unpinned); cartpole: x/th_threshold
 };
 
 __host__ __device__ inline int env_con_dim(int id, int n_surr) {
@@ -51,13 +51,14 @@ __device__ inline void env_constraints_row(const EnvParams& ep, const float* s, 
     h[1] = (float)h1;
     viol = (h0 > 0.0) || (h1 > 0.0);
     const float th = 1.48352986419518f;   // float32(85*pi/180)
-    const float xt = ep.quad_x_threshold, zt = ep.quad_z_threshold;
+    const float xt = (float)ep.thr0, zt = (float)ep.thr1;
     const bool oob = (s[0] < -xt) || (s[0] > xt) || (s[2] < -zt) || (s[2] > zt) || (s[4] < -th) || (s[4] > th);
     done = oob || viol;
   } else if (ep.id == ENV_CARTPOLE) {
-    // src/env/poles/inverted_pendulum.py:79-121, constraints.py:216-247
+    // src/env/poles/inverted_pendulum.py:11-26,79-121, constraints.py:216-247: BoundedConstraint
+    // h = x @ F^T @ A^T - b in float64 with b = [x_thr, th_thr, x_thr, th_thr]
     const double x = s[0], t = s[1];
-    const double hv[4] = {-x - 0.9, -t - 0.2, x - 0.9, t - 0.2};
+    const double hv[4] = {-x - ep.thr0, -t - ep.thr1, x - ep.thr0, t - ep.thr1};
     bool v = false;
     for (int k = 0; k < 4; ++k) {
       h[k] = (float)hv[k];

@@ -906,6 +906,15 @@ static int hb_for(int64_t n) {
   return b;
 }
 
+// LDS bytes of rollout_persist_kernel for `rpt`-row tiles (without the LDS-resident
+// actor weights)
+static size_t persist_lds_bytes(int S, int A, int Ha, int Hm, int rpt, int nw) {
+  const int S1 = S + 1;
+  const int ldx = lds_ld(S + A), ldh = lds_ld(Ha > Hm ? Ha : Hm), ldm = round_up(S1, 16) + 4, ldss = round_up(S, 4);
+  return sizeof(float) * ((size_t)rpt * (ldx + 3 * ldh + ldss + 20 + 2 * ldm + 8 + 1 + 8 + 8 + 64 + 2) + 4 +
+                          (size_t)nw * (rpt / 16) * 256 + 256);
+}
+
 // engine 2: fused-horizon kernel + count scan + ordered emit + pointer advance
 static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hipStream_t stream) {
   DRPO_REQUIRE(d->H <= PERSIST_MAX_H, "drpo_rollout: engine 2 supports horizon <= %d", PERSIST_MAX_H);
@@ -917,7 +926,7 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   a.S = S; a.A = A; a.C = d->C; a.Ha = d->Ha; a.Hm = d->Hm; a.B = B; a.H = H;
   a.ntiles = (B + rpt - 1) / rpt;
   a.env.id = d->env_id; a.env.surr_start = d->tracking_surr_start; a.env.n_surr = d->tracking_n_surr;
-  a.env.quad_x_threshold = d->quad_x_threshold; a.env.quad_z_threshold = d->quad_z_threshold;
+  a.env.thr0 = d->env_thr0; a.env.thr1 = d->env_thr1;
   a.aW1 = d->aW1; a.ab1 = d->ab1; a.aW2 = d->aW2; a.ab2 = d->ab2; a.aW3 = d->aW3; a.ab3 = d->ab3;
   a.mW1 = d->mW1; a.mb1 = d->mb1; a.mW2 = d->mW2; a.mb2 = d->mb2; a.dW1 = d->dW1; a.db1 = d->db1;
   a.dW2 = d->dW2; a.db2 = d->db2; a.lW1 = d->lW1; a.lb1 = d->lb1; a.lW2 = d->lW2; a.lb2 = d->lb2;
@@ -948,8 +957,7 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
     return (e && atoi(e) == 16) ? 16 : 8;
   }();
   const int nw = rpt == 32 ? 8 : NW;
-  const size_t lds_bytes = sizeof(float) * ((size_t)rpt * (a.ldx + 3 * a.ldh + a.lds + 20 + 2 * a.ldm + 8 + 1 + 8 + 8 +
-                                                           64 + 2) + 4 + (size_t)nw * (rpt / 16) * 256 + 256);
+  const size_t lds_bytes = persist_lds_bytes(S, A, d->Ha, d->Hm, rpt, nw);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
   // LDS-resident actor weights (see rollout_persist_kernel) when they fit
   const size_t lw_bytes = sizeof(float) * (size_t)(32 + 16 * PERSIST_L2_LDS) * 256;
@@ -1000,7 +1008,11 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
     DRPO_REQUIRE(d->tracking_surr_start + 4 * d->tracking_n_surr <= d->S, "drpo_rollout: tracking layout");
 
   RolloutWs w = rollout_ws(d->B, d->S, d->H, (char*)d->workspace);
-  const int rpt = d->rows_per_tile ? d->rows_per_tile : (d->B >= 256 * 32 ? 32 : 16);
+  // 32-row tiles halve the weight bytes per MFMA once the batch fills the chip with
+  // them (B >= 8192), when the wider tile still fits the LDS (not for tracking's S=51)
+  const int rpt = d->rows_per_tile ? d->rows_per_tile
+                                   : (d->B >= 256 * 32 && persist_lds_bytes(d->S, d->A, d->Ha, d->Hm, 32, 8) <= 160 * 1024
+                                          ? 32 : 16);
   DRPO_REQUIRE(rpt == 16 || rpt == 32, "drpo_rollout: rows_per_tile must be 16 or 32");
   const int S = d->S, A = d->A, S1 = d->S + 1;
   DRPO_REQUIRE(d->engine >= 0 && d->engine <= 2 && (d->eps_layout == 0 || d->eps_layout == 1),
@@ -1016,7 +1028,7 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
   RolloutStepArgs a{};
   a.S = S; a.A = A; a.C = d->C; a.Ha = d->Ha; a.Hm = d->Hm; a.Bmax = d->B;
   a.env.id = d->env_id; a.env.surr_start = d->tracking_surr_start; a.env.n_surr = d->tracking_n_surr;
-  a.env.quad_x_threshold = d->quad_x_threshold; a.env.quad_z_threshold = d->quad_z_threshold;
+  a.env.thr0 = d->env_thr0; a.env.thr1 = d->env_thr1;
   a.aW1 = d->aW1; a.ab1 = d->ab1; a.aW2 = d->aW2; a.ab2 = d->ab2; a.aW3 = d->aW3; a.ab3 = d->ab3;
   a.norm_mean = d->norm_mean; a.norm_std = d->norm_std; a.min_lv = d->min_lv; a.max_lv = d->max_lv;
   a.replay_states = d->replay_states; a.init_idx = d->init_idx;
@@ -1086,13 +1098,13 @@ __global__ void env_constraints_kernel(EnvParams ep, const float* s, int64_t n, 
     for (int c = 0; c < C; ++c) h[i * C + c] = hh[c];
 }
 
-DRPO_API int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, float quad_x_threshold,
-                                  float quad_z_threshold, const float* states, int64_t n, int S, uint8_t* done,
+DRPO_API int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, double env_thr0,
+                                  double env_thr1, const float* states, int64_t n, int S, uint8_t* done,
                                   uint8_t* violation, float* h, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(env_id >= 0 && env_id <= 3, "drpo_env_constraints: unknown env id %d", env_id);
   if (n == 0) return DRPO_OK;
-  EnvParams ep{env_id, tracking_surr_start, tracking_n_surr, quad_x_threshold, quad_z_threshold};
+  EnvParams ep{env_id, tracking_surr_start, tracking_n_surr, env_thr0, env_thr1};
   const int C = env_con_dim(env_id, tracking_n_surr);
   env_constraints_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ep, states, n, S, C, done, violation, h);
   DRPO_LAUNCH_CHECK("env_constraints");

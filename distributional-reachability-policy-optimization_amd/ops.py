@@ -77,12 +77,15 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
     S, A, C = alg.state_dim, alg.action_dim, alg.con_dim
     model = alg.model_ensemble
     rb, vb = alg.replay_buffer._module, alg.virt_buffer._module
-    assert B * H <= vb.capacity, 'We do not support extending by more than buffer capacity'
     _lib.require_device(policy.group.data, model.group.data, vb._states)
 
     # initial states: chronological replay indices (np.random.choice without replacement)
     if initial_states is not None:
-        src, src_ptr, src_cap = initial_states.contiguous().float(), len(initial_states), len(initial_states)
+        # the reference rolls out exactly len(initial_states) rows (src/smbpo.py:230-233)
+        src = initial_states.contiguous().float()
+        _lib.require_device(src)
+        B = len(src)
+        src_ptr = src_cap = B
         init_idx = torch.arange(B, device=dev, dtype=torch.int64)
     else:
         src, src_ptr, src_cap = rb._states, rb.pointer, rb.capacity
@@ -90,6 +93,7 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
         idx = noise.np_choice(n_real, B)
         init_idx = None if idx is None else _dev(idx, dev, torch.int64)
 
+    assert B * H <= vb.capacity, 'We do not support extending by more than buffer capacity'
     S1 = S + 1
     if noise.parity:
         ks, ns, eps_a, eps_m = _tape_rollout_noise(noise, H, B, A, S1)
@@ -120,7 +124,7 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
     d = RolloutDesc()
     d.S, d.A, d.C, d.Ha, d.Hm, d.B, d.H = S, A, C, policy.spec.dims[1], model.hidden_dim, B, H
     d.env_id, d.tracking_surr_start, d.tracking_n_surr = ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr']
-    d.quad_x_threshold, d.quad_z_threshold = ep['quad_x_threshold'], ep['quad_z_threshold']
+    d.env_thr0, d.env_thr1 = ep['thr0'], ep['thr1']
     (d.aW1, d.ab1), (d.aW2, d.ab2), (d.aW3, d.ab3) = [(W.data_ptr(), b.data_ptr()) for W, b in actor]
     (d.mW1, d.mb1), (d.mW2, d.mb2) = [(W.data_ptr(), b.data_ptr()) for W, b in trunk]
     (d.dW1, d.db1), (d.dW2, d.db2) = [(W.data_ptr(), b.data_ptr()) for W, b in diff]
@@ -154,6 +158,51 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
     view = _RolloutResult(vb, start_ptr, count)
     view.tape_counts = ns
     return view
+
+
+def rollout_host_env(alg, policy, initial_states, noise):
+    """SMBPO.rollout (src/smbpo.py:229-249) for an env WITHOUT device constraint
+    functions (envs.device_env_params returned None): the policy sample and the
+    elite-member sample run on the HIP kernels, and the env's own numpy
+    check_done / check_violation / get_constraint_values are called on the host each
+    step -- the reference's round trip (src/smbpo.py:63-65), kept only for such envs."""
+    from .buffers import ConstraintSafetySampleBuffer
+    from .torch_util import torchify
+    dev = alg.device
+    B, H = alg.rollout_batch_size, alg.horizon
+    S, A, C = alg.state_dim, alg.action_dim, alg.con_dim
+    model, env = alg.model_ensemble, alg.real_env
+    if initial_states is None:
+        real = alg.replay_buffer.get('states', device=dev)
+        idx = noise.np_choice(len(real), B)
+        if idx is None:
+            L = _lib.lib()
+            idx_t = torch.empty(B, dtype=torch.int64, device=dev)
+            _lib.check(L.drpo_sample_without_replacement(_lib.ptr(idx_t), B, len(real), noise.seed, noise.next(),
+                                                         _lib.stream()), 'sample_without_replacement')
+        else:
+            idx_t = _dev(idx, dev, torch.int64)
+        states = real.index_select(0, idx_t)
+    else:
+        states = initial_states.to(dev).float()
+        B = len(states)
+    buf = ConstraintSafetySampleBuffer(S, A, B * H, con_dim=C, device=dev)
+    for t in range(H):
+        actions = policy.act(states, eval=False, noise=noise)
+        next_states, rewards = model.sample(states, actions, noise=noise)
+        s2 = next_states.cpu().numpy()
+        dones = torchify(env.check_done(s2), to_device=False).to(dev)
+        viols = torchify(env.check_violation(s2), to_device=False).to(dev)
+        h = torchify(env.get_constraint_values(s2), to_device=False).to(dev)
+        buf.extend(states=states, actions=actions, next_states=next_states, rewards=rewards,
+                   dones=dones.reshape(-1), violations=viols.reshape(-1), constraint_values=h.reshape(len(s2), *(
+                       [] if C == 1 else [C])))
+        continues = ~dones.reshape(-1).bool()
+        if int(continues.sum()) == 0:
+            break
+        states = next_states[continues]
+    alg.virt_buffer.extend(**buf.get(as_dict=True, device=dev))
+    return buf
 
 
 class _RolloutResult:
@@ -193,8 +242,8 @@ def env_constraints(env_params, states):
     viol = torch.empty(n, dtype=torch.bool, device=states.device)
     h = torch.empty(n, C, dtype=torch.float32, device=states.device)
     _lib.check(L.drpo_env_constraints(env_params['env_id'], env_params['tracking_surr_start'],
-                                      env_params['tracking_n_surr'], env_params['quad_x_threshold'],
-                                      env_params['quad_z_threshold'], _lib.ptr(states), n, S, _lib.ptr(done),
+                                      env_params['tracking_n_surr'], env_params['thr0'],
+                                      env_params['thr1'], _lib.ptr(states), n, S, _lib.ptr(done),
                                       _lib.ptr(viol), _lib.ptr(h), _lib.stream()), 'env_constraints')
     return done, viol, (h[:, 0] if C == 1 else h)
 
@@ -236,10 +285,10 @@ def default_noise():
     return _default_noise
 
 
-def _mlp(nets, srcs, rows, trunk=False, norm=None):
+def _mlp(nets, srcs, rows, trunk=False, norm=None, nbatch=1, sstride=None):
     from .sac_step import fill_fwd
     L = _lib.lib()
-    d = fill_fwd(nets, srcs, rows, trunk=trunk, norm=norm)
+    d = fill_fwd(nets, srcs, rows, trunk=trunk, norm=norm, nbatch=nbatch, sstride=sstride)
     _lib.check(L.drpo_mlp_forward(ctypes.byref(d), _lib.stream()), 'mlp_forward')
 
 
@@ -308,21 +357,30 @@ def critic_all(critic, state, action, which=None):
     return [net.sy[-1].reshape(*lead) for net in nets]
 
 
-def constraint_critic_forward(cc, state, action, uncertainty=False, sample=False, noise=None):
+def constraint_critic_forward(cc, state, action, uncertainty=False, sample=False, noise=None, repeat=1):
     """ConstraintCritic.forward (src/ssac.py:64-92): trunk + both heads in one launch,
-    then the log-std clamp / quantile bound / clipped sample."""
+    then the log-std clamp / quantile bound / clipped sample.
+
+    repeat=K scores K action sets against the same states in ONE launch: ``action`` is
+    [K*n, A] (set-major) and the states are read K times through a zero batch stride
+    (the linear shield's candidates, src/sampling.py:430-437)."""
     assert not (uncertainty and sample), 'Uncertainty bound and sample cannot be True simultaneously.'
     L = _lib.lib()
     _lib.require_device(cc.group.data, state, action)
     s, lead = _flat2(state, state.shape[-1])
     a, _ = _flat2(action, action.shape[-1])
-    n, C = len(s), cc.output_dim
+    if repeat > 1:
+        assert len(a) == repeat * len(s), 'repeat: actions must be [repeat * n, A]'
+        lead = (len(a),)
+    n, C = len(a), cc.output_dim
+    rows = len(s)
     trunk = _net(cc.group, cc.prefix + 'trunk.', cc.trunk_spec)
     mean = _net(cc.group, cc.prefix + 'mean_head.', cc.mean_spec, n)
     nets = [trunk, mean]
     if uncertainty or sample:
         nets.append(_net(cc.group, cc.prefix + 'log_std_head.', cc.logstd_spec, n))
-    _mlp(nets, [(s, s.shape[1]), (a, a.shape[1])], n, trunk=True)
+    sstride = [0, rows * a.shape[1], 0] if repeat > 1 else None
+    _mlp(nets, [(s, s.shape[1]), (a, a.shape[1])], rows, trunk=True, nbatch=repeat, sstride=sstride)
     shape = (*lead, C) if C > 1 else tuple(lead)
     mu = mean.sy[-1]
     if not (uncertainty or sample):
@@ -338,6 +396,39 @@ def constraint_critic_forward(cc, state, action, uncertainty=False, sample=False
     if uncertainty:
         return q.reshape(shape)
     return mu.reshape(shape), sd.reshape(shape), q.reshape(shape)
+
+
+# ---------------------------------------------------------------------------
+# safety shields (src/smbpo.py:127-136, src/sampling.py:423-439)
+# ---------------------------------------------------------------------------
+SHIELD_NONE, SHIELD_THRESHOLD, SHIELD_LINEAR = 0, 1, 2
+
+
+def shield_mix(a_perf, a_safe, K=11):
+    """[K, n, A] candidates a_safe*(K-1-i)/(K-1) + a_perf*(1-(K-1-i)/(K-1))."""
+    L = _lib.lib()
+    _lib.require_device(a_perf, a_safe)
+    a_perf, a_safe = a_perf.contiguous().float(), a_safe.contiguous().float()
+    n, A = a_perf.shape
+    mixes = torch.empty(K, n, A, device=a_perf.device)
+    _lib.check(L.drpo_shield_mix(_lib.ptr(a_perf), _lib.ptr(a_safe), n, A, K, _lib.ptr(mixes), _lib.stream()),
+               'shield_mix')
+    return mixes
+
+
+def shield_select(q, mode, threshold, a_perf, a_safe, mixes=None):
+    """Per-row shield decision on the device; q [n(,C)] (mode 1) or [K*n(,C)] (mode 2)."""
+    L = _lib.lib()
+    _lib.require_device(q, a_perf, a_safe)
+    a_perf, a_safe = a_perf.contiguous().float(), a_safe.contiguous().float()
+    n, A = a_perf.shape
+    K = 1 if mixes is None else mixes.shape[0]
+    q = q.contiguous().float()
+    C = q.numel() // (K * n) if mode == SHIELD_LINEAR else q.numel() // max(n, 1)
+    out = torch.empty_like(a_perf)
+    _lib.check(L.drpo_shield_select(_lib.ptr(q), K, n, max(C, 1), A, mode, float(threshold), _lib.ptr(a_perf),
+                                    _lib.ptr(a_safe), _lib.ptr(mixes), _lib.ptr(out), _lib.stream()), 'shield_select')
+    return out
 
 
 def multiplier_forward(mult, state, Qc):

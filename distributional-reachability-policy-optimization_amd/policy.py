@@ -2,6 +2,7 @@
 
 The MLP S->H..->2A (ReLU) lives in a flat parameter group; ``act`` runs the fused
 HIP MLP forward + squashed-Gaussian head (see ops.py)."""
+import numpy as np
 import torch
 
 from .params import FlatGroup, MLPSpec
@@ -69,8 +70,35 @@ class SquashedGaussianPolicy(Module):
         mu, std = ops.policy_params(self, states)
         return td.Independent(SquashedGaussian(mu, std), 1)
 
-    def act1(self, state, eval=False):
-        return self.act(torch.unsqueeze(state, 0), eval)[0]
+    def act1(self, state, eval=False, noise=None):
+        return self.act(torch.unsqueeze(state, 0), eval, noise)[0]
 
     def copy_from(self, other):
         self.group.data.copy_(other.group.data)
+
+
+class UniformPolicy:
+    """Warm-up policy (src/policy.py:20-58): a ~ U[low, high) per action dim, drawn on
+    the device (or taken from a recorded tape in parity mode)."""
+
+    def __init__(self, env_or_action_space, device=None, noise=None):
+        space = getattr(env_or_action_space, 'action_space', env_or_action_space)
+        from .torch_util import device as default_device
+        self.device = default_device if device is None else device
+        self.low = torch.as_tensor(np.asarray(space.low, np.float32), device=self.device)
+        self.high = torch.as_tensor(np.asarray(space.high, np.float32), device=self.device)
+        self.shape = list(space.shape)
+        self.noise = noise
+
+    def act(self, states, eval, noise=None):
+        noise = noise or self.noise
+        n = len(states)
+        u = None if noise is None else noise.rand((n, *self.shape))
+        if u is None:
+            u = torch.rand(n, *self.shape, device=self.device)
+        else:
+            u = torch.from_numpy(u).to(self.device)
+        return self.low + u * (self.high - self.low)
+
+    def act1(self, state, eval=False, noise=None):
+        return self.act(torch.unsqueeze(state, 0), eval, noise)[0]

@@ -14,20 +14,50 @@ import random
 import numpy as np
 
 
+def _mix64(x):
+    """splitmix64 finaliser: decorrelates Philox keys derived from (seed, rank)."""
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
 class DeviceNoise:
+    """Production noise.
+
+    * Device draws (Philox4x32-10) are keyed by ``seed``: the base seed on rank 0 and
+      a splitmix64 mix of (base seed, rank) on the other data-parallel ranks, so each
+      rank draws its own minibatches, initial states and Gaussian noise.
+    * Host choices the reference makes with Python's ``random`` (elite member per
+      rollout step, src/dynamics.py:199; critic pick, src/ssac.py:43) come from a
+      private ``random.Random(base seed)`` that is identical on every rank: all
+      replicas pick the same member / critic, so the mean-all-reduced gradient is
+      the gradient of one well-defined loss.
+
+    ``seed=None`` takes ``torch.initial_seed()`` (what set_seed / torch.manual_seed
+    set, src/util.py:11-17); ``rank=None`` takes the torch.distributed rank."""
     parity = False
 
-    def __init__(self, seed=0):
-        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    def __init__(self, seed=None, rank=None):
+        if seed is None:
+            import torch
+            seed = torch.initial_seed()
+        if rank is None:
+            from .distributed import rank as dist_rank
+            rank = dist_rank()
+        self.base_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.rank = int(rank)
+        self.seed = self.base_seed if self.rank == 0 else _mix64(self.base_seed ^ _mix64(self.rank))
+        self.host = random.Random(self.base_seed)
         self.ctr = 0
 
     def next(self):
         self.ctr += 1
         return self.ctr
 
-    # reference host-RNG call sites
+    # reference host-RNG call sites (shared across ranks)
     def choice(self, n):
-        return random.choice(range(n))
+        return self.host.choice(range(n))
 
     # device-drawn sites: nothing to hand over
     def np_choice(self, high, size):
@@ -43,6 +73,9 @@ class DeviceNoise:
         return None
 
     def randint(self, high, n):
+        return None
+
+    def rand(self, shape):
         return None
 
 
@@ -95,6 +128,9 @@ class TapeNoise:
 
     def randint(self, high, n):
         return np.asarray(self._take('randint', (n,)), dtype=np.int64)
+
+    def rand(self, shape):
+        return np.ascontiguousarray(self._take('rand', shape), dtype=np.float32)
 
     def done(self):
         return self.pos == len(self.entries)

@@ -426,7 +426,7 @@ class SACEngine:
             dm = self.buf('c.dm', B, dtype=torch.uint8)
             ep = self.env_params
             _lib.check(L.drpo_env_constraints(ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr'],
-                                              ep['quad_x_threshold'], ep['quad_z_threshold'], s2c.data_ptr(), B, S,
+                                              ep['thr0'], ep['thr1'], s2c.data_ptr(), B, S,
                                               dm.data_ptr(), self.buf('c.vm', B, dtype=torch.uint8).data_ptr(),
                                               self.buf('c.hm', B, C).data_ptr(), _lib.stream()), 'env_constraints')
         xs = self.buf('c.x', B, S + A)

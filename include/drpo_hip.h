@@ -60,7 +60,8 @@ int drpo_event_elapsed_ms(float* ms /* host */, void* start, void* stop);
 typedef struct {
   int S, A, C, Ha, Hm, B, H;
   int env_id, tracking_surr_start, tracking_n_surr;
-  float quad_x_threshold, quad_z_threshold;
+  double env_thr0, env_thr1;     /* quadrotor: x/z_threshold (safe-control-gym); cartpole: x_threshold,
+                                    th_threshold (SafeInvertedPendulumEnv); unused otherwise */
   const float *aW1, *ab1, *aW2, *ab2, *aW3, *ab3;          /* actor: packed weight mirrors + biases */
   const float *mW1, *mb1, *mW2, *mb2, *dW1, *db1, *dW2, *db2, *lW1, *lb1, *lW2, *lb2; /* ensemble: packed mirrors [E] (member stride drpo_packed_size) + biases [E][out] */
   const float *norm_mean, *norm_std, *min_lv, *max_lv;
@@ -90,9 +91,22 @@ int drpo_rollout(const drpo_rollout_desc_t* d /* host */, drpo_stream_t stream);
 
 /* batched env constraint functions, e.g. PointRobot.get_constraint_values /
  * check_violation / check_done (src/env/point_robot.py:96-131); h is [n][C] */
-int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, float quad_x_threshold,
-                         float quad_z_threshold, const float* states, int64_t n, int S, uint8_t* done,
+int drpo_env_constraints(int env_id, int tracking_surr_start, int tracking_n_surr, double env_thr0,
+                         double env_thr1, const float* states, int64_t n, int S, uint8_t* done,
                          uint8_t* violation, float* h, drpo_stream_t stream);
+
+/* ---------------------------------------------------------------- safety shields
+ * Real-env step shield (SMBPO.step_generator, src/smbpo.py:127-136) and the
+ * evaluation shields of sample_episodes_batched (src/sampling.py:423-439).
+ * drpo_shield_mix writes the linear shield's K candidate actions
+ * mix_i = a_safe*(K-1-i)/(K-1) + a_perf*(1-(K-1-i)/(K-1)) as [K][n][A] (scored by one
+ * constraint-critic forward over K*n rows); drpo_shield_select picks per row:
+ * mode 0 a_perf; mode 1 a_safe where max_C q > threshold (q [n][C]); mode 2 linear
+ * shield: a_safe, overridden by mix_i wherever max_C q_i <= threshold (q [K][n][C]). */
+int drpo_shield_mix(const float* a_perf, const float* a_safe, int64_t n, int A, int K, float* mixes,
+                    drpo_stream_t stream);
+int drpo_shield_select(const float* q, int K, int64_t n, int C, int A, int mode, float threshold, const float* a_perf,
+                       const float* a_safe, const float* mixes, float* out, drpo_stream_t stream);
 
 /* B distinct indices in [0, N): production stand-in for random_choice(replace=False)
  * (src/torch_util.py:41-48) */

@@ -26,7 +26,7 @@ def main():
     dev = torch.device('cuda')
     B = args.batch
     alg = bench.make_alg(dev, B, 10, 7, 0, bench.QUAD_JSON)
-    rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
+    rep = bench.synth_replay('quadrotor', 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)
@@ -59,7 +59,7 @@ def host_vs_gpu(steps=20):
     import bench
     dev = torch.device('cuda')
     alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON)
-    rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
+    rep = bench.synth_replay('quadrotor', 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)

@@ -65,7 +65,7 @@ def rollout_stamps():
     L.drpo_debug_stamps_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device('cuda')
     alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON)
-    rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
+    rep = bench.synth_replay('quadrotor', 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)
@@ -97,7 +97,7 @@ def fused_stamps():
     dev = torch.device('cuda')
     hm = int(os.environ.get('DRPO_STAMPS_HM', '200'))   # model width (200 = reference; else the unpaired path)
     alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON, extra={'model_cfg': {'hidden_dim': hm}})
-    rep = bench.synth_replay(12, 2, 2, 100000, np.random.RandomState(0))
+    rep = bench.synth_replay('quadrotor', 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)

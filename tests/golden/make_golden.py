@@ -412,6 +412,119 @@ def gen_smbpo_update(out, name, seed):
     np.savez_compressed(os.path.join(out, f'smbpo_update_{name}.npz'), **d)
 
 
+class RecordingPointRobot(PointRobot):
+    """The reference PointRobot whose training-env resets (global np.random.uniform,
+    src/env/point_robot.py:44-47) are recorded so the test-side env can replay them."""
+    resets = []
+
+    def reset(self):
+        obs = super().reset()
+        if self.id is None:
+            RecordingPointRobot.resets.append(np.array(self.state, dtype=np.float64))
+        return obs
+
+
+def trainer_config(seed_cfg):
+    cfg = small_config('point-robot', B=32, H=3, sac_batch=32)
+    cfg.update({'buffer_min': 40, 'steps_per_epoch': 10, 'model_update_period': 4, 'model_initial_steps': 5,
+                'model_steps': 3, 'safe_shield': True, 'safe_shield_threshold': seed_cfg['shield'],
+                'eval_shield_threshold': seed_cfg['eval_shield'], 'eval_shield_type': 'linear', 'mode': 'train'})
+    return cfg
+
+
+def gen_trainer(out, seed, shield=-0.1, eval_shield=-0.05):
+    """main.py's loop shape (main.py:50-62): setup() -> evaluate() -> epoch() ->
+    evaluate() on point-robot, with every random draw recorded. Shield decisions are
+    discrete, so the generator also records how close each shield query came to its
+    threshold (the parity test needs a margin well above fp32 noise)."""
+    import src.ssac as ssac_mod
+    from src.log import default_log as rlog
+    cfg = trainer_config({'shield': shield, 'eval_shield': eval_shield})
+    RecordingPointRobot.resets = []
+    set_seed(seed)
+    factory = lambda id=None: TorchWrapper(RecordingPointRobot(id=id))  # noqa: E731
+    data = CheckpointableData()
+    alg = SMBPO(cfg, factory, data, 1)
+    d = meta('point-robot', cfg, alg)
+    d.update(sd_dict(alg, 'sd0/'))
+    d['sd0/log_alpha'] = t2n(alg.solver.log_alpha)
+    d['cfg/buffer_min'], d['cfg/steps_per_epoch'] = np.array(cfg.buffer_min), np.array(cfg.steps_per_epoch)
+    d['cfg/model_update_period'] = np.array(cfg.model_update_period)
+    d['cfg/model_initial_steps'], d['cfg/model_steps'] = np.array(cfg.model_initial_steps), np.array(cfg.model_steps)
+    d['cfg/shield'], d['cfg/eval_shield'] = np.array(shield), np.array(eval_shield)
+    margins = {'step': [], 'eval': []}
+    orig_get_qc = ssac_mod.SSAC._get_qc
+
+    def rec_get_qc(self, q):
+        out_q = orig_get_qc(self, q)
+        n = out_q.reshape(-1).shape[0]
+        if n == 1:
+            margins['step'].append(float((out_q - shield).abs().min()))
+        elif n == 10:
+            margins['eval'].append(float((out_q - eval_shield).abs().min()))
+        return out_q
+    ssac_mod.SSAC._get_qc = rec_get_qc
+    try:
+        with Tape() as tp:
+            alg.setup()
+        d.update(tp.to_npz_dict('setup_tape'))
+        ev0 = alg.evaluate()
+        with Tape() as tp:
+            alg.epoch()
+        d.update(tp.to_npz_dict('epoch_tape'))
+        ev1 = alg.evaluate()
+    finally:
+        ssac_mod.SSAC._get_qc = orig_get_qc
+    keys = sorted(ev0)
+    d['eval/keys'] = np.array(keys)
+    d['eval/0'] = np.array([ev0[k] for k in keys])
+    d['eval/1'] = np.array([ev1[k] for k in keys])
+    d['resets'] = np.stack(RecordingPointRobot.resets)
+    d['margin/step'] = np.array(margins['step'] or [np.inf])
+    d['margin/eval'] = np.array(margins['eval'] or [np.inf])
+    d.update(sd_dict(alg, 'sd1/'))
+    d['sd1/log_alpha'] = t2n(alg.solver.log_alpha)
+    for name, buf in (('replay', alg.replay_buffer), ('virt', alg.virt_buffer)):
+        d[f'{name}/n'] = np.array(len(buf))
+        for k, v in buf.get(as_dict=True).items():
+            d[f'{name}/{k}'] = t2n(v)
+    dk = sorted(data._data)
+    d['data/keys'] = np.array(dk)
+    for i, k in enumerate(dk):
+        d[f'data/{i:03d}'] = np.array([np.nan if v is None else float(v) for v in data[k]], dtype=np.float64)
+    d['episodes_csv'] = np.array(open(os.path.join(str(rlog.dir), 'episodes.csv')).read())
+    print('trainer fixture: min shield margins step %.3g eval %.3g, %d real steps, eval %s / %s' % (
+        d['margin/step'].min(), d['margin/eval'].min(), len(alg.replay_buffer), ev0, ev1))
+    np.savez_compressed(os.path.join(out, 'trainer_point-robot.npz'), **d)
+    return float(min(d['margin/step'].min(), d['margin/eval'].min()))
+
+
+def gen_checkpoint(out, seed):
+    """A ckpt_{epoch}.pt / data.pt pair written by the reference's own Checkpointer
+    (src/checkpoint.py:55-83, main.py:34-35,67-71) from a point-robot SMBPO after a
+    short fit + rollout_and_update, stored as raw bytes for the interop test."""
+    import io
+    from src.checkpoint import Checkpointer
+    cfg = small_config('point-robot', B=32, H=3, sac_batch=32)
+    alg = build_alg('point-robot', cfg, seed)
+    fill_replay(alg, 'point-robot', 300, seed + 1, alg.con_dim)
+    alg.update_models(3)
+    alg.rollout_and_update()
+    alg.epochs_completed += 3
+    data = alg.data
+    data.append('critic loss', float(alg.recent_critic_losses[-1]))
+    data.append('eval return mean', 1.25)
+    tmp = tempfile.mkdtemp()
+    Checkpointer(alg, tmp, 'ckpt_{}.pt').save(3)
+    Checkpointer(data, tmp, 'data.pt').save()
+    d = meta('point-robot', cfg, alg)
+    d['ckpt_bytes'] = np.frombuffer(open(os.path.join(tmp, 'ckpt_3.pt'), 'rb').read(), dtype=np.uint8)
+    d['data_bytes'] = np.frombuffer(open(os.path.join(tmp, 'data.pt'), 'rb').read(), dtype=np.uint8)
+    d.update(sd_dict(alg, 'sd/'))
+    d['log_alpha'] = t2n(alg.solver.log_alpha)
+    np.savez_compressed(os.path.join(out, 'checkpoint_point-robot.npz'), **d)
+
+
 def gen_init_hashes(out):
     """sha256 of every state_dict tensor of a DEFAULT-width SMBPO (quadrotor dims, E=7)
     for seed 0: pins the build's reference-order initialisation bit-exactly."""
@@ -432,6 +545,13 @@ def main():
     out = HERE
     tmp = tempfile.mkdtemp()
     default_log.setup(tmp)
+    if sys.argv[1:2] == ['trainer']:
+        seed = int(sys.argv[2]) if len(sys.argv) > 2 else 55
+        gen_trainer(out, seed)
+        return
+    if sys.argv[1:] == ['checkpoint']:
+        gen_checkpoint(out, 61)
+        return
     if sys.argv[1:] == ['robust']:
         gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
         gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
@@ -449,6 +569,8 @@ def main():
     gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
     gen_smbpo_update(out, 'point-robot', 41)
     gen_smbpo_update(out, 'quadrotor', 42)
+    gen_trainer(out, 55)
+    gen_checkpoint(out, 61)
     print('golden fixtures written to', out)
 
 

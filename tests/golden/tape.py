@@ -9,6 +9,7 @@ While active, it wraps the random sources the reference's hot path draws from
   torch.randint(...)            -> src/sampling.py:148, src/dynamics.py:166,174
   random.choice(seq)            -> src/dynamics.py:199, src/ssac.py:43
   np.random.choice(...)         -> src/torch_util.py:44
+  torch.rand(...)               -> UniformPolicy.act (src/policy.py:43-47, warm-up)
 
 Every wrapper leaves the generator consumption and the returned value exactly
 as the original (the reference runs unmodified); it only records the standard
@@ -57,6 +58,11 @@ class Tape:
         self.entries.append(('randint', out.numpy().copy()))
         return out
 
+    def _rand(self, *args, **kwargs):
+        out = _orig['rand'](*args, **kwargs)
+        self.entries.append(('rand', out.detach().numpy().copy()))
+        return out
+
     def _choice(self, seq):
         idx = _orig['choice'](range(len(seq)))
         self.entries.append(('choice', np.array(idx, dtype=np.int64)))
@@ -69,11 +75,13 @@ class Tape:
 
     def __enter__(self):
         _orig.update(normal=torch.normal, normal_=torch.Tensor.normal_, randn_like=torch.randn_like,
-                     randint=torch.randint, choice=random.choice, np_choice=np.random.choice)
+                     randint=torch.randint, choice=random.choice, np_choice=np.random.choice,
+                     rand=torch.rand)
         torch.normal = self._normal
         torch.Tensor.normal_ = lambda t, *a, **k: self._normal_(t, *a, **k)
         torch.randn_like = self._randn_like
         torch.randint = self._randint
+        torch.rand = self._rand
         random.choice = self._choice
         np.random.choice = self._np_choice
         self.active = True
@@ -84,6 +92,7 @@ class Tape:
         torch.Tensor.normal_ = _orig['normal_']
         torch.randn_like = _orig['randn_like']
         torch.randint = _orig['randint']
+        torch.rand = _orig['rand']
         random.choice = _orig['choice']
         np.random.choice = _orig['np_choice']
         self.active = False

@@ -1,0 +1,254 @@
+"""HIP path vs the CPU oracle at the EXACT BASELINE config shapes:
+
+  config 2  quadrotor    E=7  H=10 B=4096
+  config 3  point-robot  E=7  H=20 B=8192
+  config 4  tracking     E=8  H=40 B=16384
+  config 5  quadrotor    E=32 H=80 B=65536   (global batch, on one GPU here)
+
+Per config, with reference default widths (actor/critics 256, model 200) and the
+env's reference JSON hyper-parameters:
+
+* a full rollout (B x H) by the production fused-horizon engine vs the oracle driven
+  by live reference RNG calls (the recorded draws re-indexed by original row).
+  Regime: the diff head's state rows are scaled by 1e-3 (the reward row keeps full
+  scale, so the whole member MLP is exercised through it) and the log-var bias is
+  -20 (std clamps to e^-5): trajectories drift slowly and (almost) no row finishes,
+  so a threshold-straddling fp32 rounding -- which at 5.2 M transitions with rows
+  dying every step would flip some done flag -- is practically excluded; the row
+  count must still equal the oracle's exactly;
+* the same shape with the raw random weights (rows die every step): structural
+  properties of the HIP output (per-step survivor chaining in reference order,
+  flags == the env constraint functions of next_state, action bounds);
+* one update_critic + update_actor_and_alpha + update_multiplier at the full B vs
+  the oracle with its draws replayed;
+* a full-width (hidden 200) fit(steps=3) at the config's E vs the oracle.
+
+Tolerances (fp32): rollout floats |d| <= 2e-4 + 2e-4|ref|; violation flags exact
+except where the oracle's constraint value is within 1e-5 of 0 (the flag is that
+value's sign); losses rtol 1e-4 (2e-4 at B=65536); parameters after one Adam step
+|d| <= 3e-5 + 1e-4|ref|; fit losses rtol 1e-4, fit parameters |d| <= 5e-5 + 2e-4|ref|,
+elites exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import drpo_amd
+from fake_envs import ENVS
+from gpu_helpers import DEV, COMP
+from oracle import drpo_oracle as O
+from test_gpu_rollout import original_row_tape
+
+pytestmark = pytest.mark.gpu
+
+CFGS = [2, 3, 4, 5]
+
+
+def _alg(c, B=None, seed=5):
+    cd = bench.CONFIGS[c]
+    env = cd['env']
+    B = B or cd['B']
+    torch.manual_seed(seed)
+    alg = bench.make_alg(DEV, B, cd['H'], cd['E'], seed, bench.ENV_JSON[env], env=env)
+    return alg, cd
+
+
+def _oracle_threads():
+    torch.set_num_threads(max(4, min(16, torch.get_num_threads() * 4)))
+
+
+def _fill(alg, env, N, seed):
+    rep = bench.synth_replay(env, N, np.random.RandomState(seed))
+    alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(DEV) for k, v in rep.items()})
+    return rep
+
+
+def _close(got, ref, tol, msg):
+    g = got.detach().cpu().numpy() if torch.is_tensor(got) else np.asarray(got)
+    r = ref.detach().cpu().numpy() if torch.is_tensor(ref) else np.asarray(ref)
+    assert g.shape == r.shape, (msg, g.shape, r.shape)
+    bad = np.abs(g.astype(np.float64) - r) > tol + tol * np.abs(r)
+    assert not bad.any(), (msg, int(bad.sum()), float(np.abs(g - r).max()))
+
+
+@pytest.mark.parametrize('c', CFGS)
+def test_config_rollout_vs_oracle(c):
+    alg, cd = _alg(c)
+    env, B, H = cd['env'], cd['B'], cd['H']
+    rep = _fill(alg, env, 100000, 3)
+    m = alg.model_ensemble
+    st = torch.from_numpy(rep['states'])
+    mean, std = O.normalizer_fit(st)
+    m.state_normalizer.mean.copy_(mean)
+    m.state_normalizer.std.copy_(std)
+    _, diff, logv = m.views()
+    S = alg.state_dim
+    diff[-1][0][:, :S].mul_(1e-3)
+    diff[-1][1][:, :S].mul_(1e-3)
+    logv[-1][1].fill_(-20.0)
+    E = m.ensemble_size
+    m._elite_inds = sorted({0, E // 2, E - 1, 1, E - 2})[:min(5, E)]
+    sd = {k: v.detach().cpu() for k, v in alg.state_dict().items()}
+    P = {k[len('solver.'):]: v for k, v in sd.items() if k.startswith('solver.actor.')}
+    P.update({k: v for k, v in sd.items() if k.startswith('model_ensemble.')})
+    _oracle_threads()
+    torch.manual_seed(c)
+    live = O.LiveRNG()
+    ref = O.rollout(P, 'actor.net.', 'model_ensemble.', m._elite_inds, st, env, B, H, live)
+    n = len(ref['states'])
+    assert n >= 0.95 * B * H, 'regime: (almost) no row may finish'
+    tape = drpo_amd.TapeNoise(original_row_tape(live.entries, ref, B))
+    del live
+    from drpo_amd import ops
+    out = ops.rollout(alg, alg.actor, None, tape, eps_layout=1)
+    torch.cuda.synchronize()
+    assert tape.done()
+    assert len(out) == n
+    got = out.get(as_dict=True)
+    for k in ('states', 'actions', 'next_states', 'rewards', 'constraint_values'):
+        _close(got[k], ref[k].reshape(got[k].shape), 2e-4, f'config {c} {k}')
+    assert torch.equal(got['dones'].cpu(), ref['dones'])
+    hv = ref['constraint_values'].reshape(n, -1)
+    marginal = (hv.abs() < 1e-5).any(1)
+    vg, vr = got['violations'].cpu(), ref['violations']
+    assert torch.equal(vg[~marginal], vr[~marginal]), f'config {c} violations'
+
+
+@pytest.mark.parametrize('c', CFGS)
+def test_config_rollout_dying_rows_properties(c):
+    """Raw random weights: rows finish at every step. The output must chain: step t+1's
+    states are step t's next_states of the rows that did not finish, in order."""
+    alg, cd = _alg(c, seed=7)
+    env, B, H = cd['env'], cd['B'], cd['H']
+    _fill(alg, env, 100000, 4)
+    m = alg.model_ensemble
+    m.state_normalizer.fit(alg.replay_buffer.get('states'))
+    m._elite_inds = list(range(min(5, m.ensemble_size)))
+    out = alg.rollout(alg.actor, noise=drpo_amd.DeviceNoise(99, rank=0))
+    torch.cuda.synchronize()
+    n = len(out)
+    got = out.get(as_dict=True)
+    assert B <= n <= B * H
+    d = got['dones'].cpu().numpy()
+    start, alive = 0, B
+    steps = 0
+    while start < n:
+        seg = slice(start, start + alive)
+        nd = ~d[seg]
+        nxt = int(nd.sum())
+        if start + alive < n:
+            assert torch.equal(got['states'][start + alive:start + alive + nxt], got['next_states'][seg][nd]), \
+                f'step {steps} survivors'
+        start += alive
+        alive = nxt
+        steps += 1
+        if alive == 0:
+            break
+    assert start == n and steps <= H
+    from drpo_amd import ops
+    dn, vl, h = ops.env_constraints(alg.env_params, got['next_states'])
+    assert torch.equal(dn, got['dones']) and torch.equal(vl, got['violations'])
+    assert torch.equal(h, got['constraint_values'])
+    assert (got['actions'].abs() <= 1).all() and torch.isfinite(got['next_states']).all()
+
+
+def _sac_batch(alg, env, jsn, B, seed):
+    rng = np.random.RandomState(seed)
+    rep = bench.synth_replay(env, 20000, rng, DEV, alg.env_params)
+    idx = rng.randint(0, 20000, B)
+    C = alg.con_dim
+    h = torch.from_numpy(rep['constraint_values'])[idx].reshape(B, -1) * jsn.get('constraint_scale', 10.0)
+    h = h + (h > 0).float() * jsn.get('constraint_offset', 0.0)
+    d = torch.from_numpy(rep['dones'])[idx]
+    batch = (torch.from_numpy(rep['states'])[idx], torch.from_numpy(rep['actions'])[idx],
+             torch.from_numpy(rep['next_states'])[idx],
+             torch.from_numpy(rep['rewards'])[idx] * jsn['reward_scale'] + jsn['alive_bonus'],
+             d, torch.from_numpy(rep['violations'])[idx], h if C > 1 else h[:, 0])
+    return batch
+
+
+def _check_params(sol, P, msg, atol=3e-5, rtol=1e-4):
+    sd = sol.state_dict()
+    bad = []
+    for k, exp in P.items():
+        if k not in sd:
+            continue
+        got, e = sd[k].detach().cpu().numpy(), exp.numpy()
+        err = np.abs(got - e) - (atol + rtol * np.abs(e))
+        if (err > 0).any():
+            bad.append((k, float(np.abs(got - e).max()), int((err > 0).sum()), e.size))
+    assert not bad, f'{msg}: {bad[:6]}'
+
+
+@pytest.mark.parametrize('c', CFGS)
+def test_config_sac_update_vs_oracle(c):
+    alg, cd = _alg(c)
+    env, B = cd['env'], cd['B']
+    jsn = bench.ENV_JSON[env]
+    sol = alg.solver
+    S, A, C = alg.state_dim, alg.action_dim, alg.con_dim
+    sd = {k: v.detach().cpu().clone() for k, v in alg.state_dict().items()}
+    Ps = {k[len('solver.'):]: v for k, v in sd.items() if k.startswith('solver.') and
+          not k.startswith('solver.model_ensemble') and k != 'solver.total_updates'}
+    sc = jsn['sac_cfg']
+    orc = O.SSACOracle(Ps, dict(batch_size=B, target_entropy=sc['target_entropy'], penalty_lb=sc['penalty_lb'],
+                                penalty_ub=sc['penalty_ub'], actor_lr=sc['actor_lr'], actor_lr_end=sc['actor_lr_end'],
+                                std_ratio=sc['constraint_critic_cfg']['std_ratio'],
+                                updates_per_training=sol.updates_per_training), C, A)
+    batch = _sac_batch(alg, env, jsn, B, 4)
+    dev_batch = [x.to(DEV) for x in batch]
+    rtol = 2e-4 if B > 32768 else 1e-4
+    _oracle_threads()
+    torch.manual_seed(c)
+    live = O.LiveRNG()
+    lq_ref, lqc_ref = orc.update_critic(*batch, live)
+    tape = drpo_amd.TapeNoise(live.entries)
+    lq, lqc = sol.update_critic(*dev_batch, noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    np.testing.assert_allclose(lq.item(), float(lq_ref), rtol=rtol)
+    np.testing.assert_allclose(lqc.item(), float(lqc_ref), rtol=rtol)
+    _check_params(sol, orc.P, f'config {c} after update_critic')
+    live = O.LiveRNG()
+    orc.update_actor_and_alpha(batch[0], live)
+    tape = drpo_amd.TapeNoise(live.entries)
+    sol.update_actor_and_alpha(dev_batch[0], noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    np.testing.assert_allclose(sol.log_alpha.item(), float(orc.log_alpha), rtol=1e-5, atol=1e-6)
+    _check_params(sol, orc.P, f'config {c} after update_actor_and_alpha')
+    live = O.LiveRNG()
+    orc.update_multiplier(batch[0], live)
+    tape = drpo_amd.TapeNoise(live.entries)
+    sol.update_multiplier(dev_batch[0], noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    _check_params(sol, orc.P, f'config {c} after update_multiplier')
+
+
+@pytest.mark.parametrize('c', CFGS)
+def test_config_full_width_fit_vs_oracle(c):
+    alg, cd = _alg(c, B=256)
+    env = cd['env']
+    m = alg.model_ensemble
+    assert m.hidden_dim == 200 and m.ensemble_size == cd['E']
+    _fill(alg, env, 30000, 6)
+    buf = {k: v.cpu() for k, v in alg.replay_buffer.get(as_dict=True).items()}
+    P = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    _oracle_threads()
+    torch.manual_seed(c)
+    live = O.LiveRNG()
+    opt = {}
+    ref_losses, ref_elites = O.ens_fit(P, '', opt, buf, 3, m.ensemble_size, m.batch_size, m.holdout_size,
+                                       m.num_elites, live)
+    tape = drpo_amd.TapeNoise(live.entries)
+    losses = m.fit(alg.replay_buffer, steps=3, noise=tape)
+    assert tape.done()
+    np.testing.assert_allclose(losses, ref_losses, rtol=1e-4)
+    assert m._elite_inds == ref_elites
+    sd = m.state_dict()
+    for k in O.ens_param_keys(P, ''):
+        got, e = sd[k].cpu().numpy(), P[k].numpy()
+        err = np.abs(got - e) - (5e-5 + 2e-4 * np.abs(e))
+        assert not (err > 0).any(), (k, float(np.abs(got - e).max()))

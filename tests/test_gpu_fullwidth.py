@@ -42,7 +42,7 @@ def test_full_width_sac_updates_vs_oracle():
     orc = O.SSACOracle(Ps, dict(batch_size=B, target_entropy=-2.0, penalty_lb=-1.0, actor_lr=1e-4,
                                 updates_per_training=sol.updates_per_training), 2, 2)
     rng = np.random.RandomState(4)
-    rep = bench.synth_replay(12, 2, 2, 4000, rng)
+    rep = bench.synth_replay('quadrotor', 4000, rng)
     idx = rng.randint(0, 4000, B)
     h = torch.from_numpy(rep['constraint_values'])[idx]
     batch = (torch.from_numpy(rep['states'])[idx], torch.from_numpy(rep['actions'])[idx],

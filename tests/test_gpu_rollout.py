@@ -148,7 +148,7 @@ def test_fused_engine_matches_step_engine_device_noise(B, H, rpt):
     for engine in (1, 2):
         random.seed(11)
         alg = bench.make_alg(DEV, B, H, 7, 0, bench.QUAD_JSON)
-        rep = bench.synth_replay(12, 2, 2, 20000, np.random.RandomState(0))
+        rep = bench.synth_replay('quadrotor', 20000, np.random.RandomState(0))
         alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(DEV) for k, v in rep.items()})
         alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
         bench.steady_mode(alg)
