@@ -421,6 +421,7 @@ def adam_update(opt, key, param, grad, lr, weight_decay, betas=(0.9, 0.999), eps
     st['step'] += 1
     if weight_decay != 0:
         grad = grad.add(param, alpha=weight_decay)
+    st['g'] = grad       # tests: the effective (clipped + L2) gradient of this step
     st['m'].lerp_(grad, 1 - betas[0])
     st['v'].mul_(betas[1]).addcmul_(grad, grad, value=1 - betas[1])
     step = float(st['step'])
@@ -538,7 +539,10 @@ class SSACOracle:
             loss = loss_fn(Q)
             grads = torch.autograd.grad(loss, [params[k] for k in keys], allow_unused=True)
         # params outside the graph keep grad=None: torch's clip and Adam skip them
-        return loss.detach(), {k: g.clone() for k, g in zip(keys, grads) if g is not None}
+        out = {k: g.clone() for k, g in zip(keys, grads) if g is not None}
+        self.last_grads = getattr(self, 'last_grads', {})
+        self.last_grads.update(out)      # tests: conditioning of each element's Adam step
+        return loss.detach(), out
 
     @property
     def alpha(self):
