@@ -42,7 +42,6 @@ class GradReducer:
     def __init__(self, group=None):
         self.group = group
         self.world = world_size()
-        self.avg_op = self.world > 1 and _dist.get_backend(group) == 'nccl'
 
     @property
     def active(self):
@@ -51,14 +50,13 @@ class GradReducer:
     def mean_(self, *tensors):
         if self.world == 1:
             return
+        # sum + scale on every backend (RCCL and gloo run the same code path; the
+        # scale is one elementwise pass over <= 1.5 MB)
         for t in tensors:
             if t is None:
                 continue
-            if self.avg_op:
-                _dist.all_reduce(t, op=_dist.ReduceOp.AVG, group=self.group)
-            else:
-                _dist.all_reduce(t, group=self.group)
-                t.div_(self.world)
+            _dist.all_reduce(t, group=self.group)
+            t.div_(self.world)
 
     def broadcast_(self, *tensors, src=0):
         if self.world == 1:
@@ -142,7 +140,7 @@ class MemberShard:
         """t [E, ...]: every rank's own slice -> replicated on all ranks (in place)."""
         if self.world == 1:
             return t
-        if self.even and _dist.get_backend(self.group) == 'nccl':
+        if self.even:          # one collective (RCCL and gloo alike)
             own = t[self.z0:self.z1].clone()
             _dist.all_gather_into_tensor(t, own, group=self.group)
         else:
