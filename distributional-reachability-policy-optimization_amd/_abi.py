@@ -82,8 +82,9 @@ PROTOTYPES = {
                                 P, P]),
     'drpo_ens_head': (c_int, [P, P, P, c_int64, c_int64, c_int, c_int, P, P, P, P, c_uint64, c_uint64, P, P, P, P,
                               P]),
+    'drpo_ens_loss_workspace_size': (c_size_t, [c_int64, c_int, c_int]),
     'drpo_ens_loss': (c_int, [P, P, P, c_int64, P, c_int64, c_int64, c_int, c_int, P, P, c_float, P, P, P, P, P, P,
-                              P, P]),
+                              P, P, P]),
 }
 
 

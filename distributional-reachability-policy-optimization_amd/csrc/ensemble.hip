@@ -40,12 +40,21 @@ __device__ __forceinline__ int64_t chrono_to_phys(int64_t j, int64_t ptr, int64_
 // ---------------------------------------------------------------------------
 // gather
 // ---------------------------------------------------------------------------
+// One thread per gathered ELEMENT (row x [s | a | s' | r] column): the replay rows
+// are random, so the copy is latency-bound; spreading it over rows * (2S+A+1)
+// threads (instead of one thread per row walking its 2S+A+1 columns) keeps the whole
+// chip's memory pipes busy. Each thread derives its row's index itself (recorded,
+// or the row's Philox draw -- the same value for every column of the row).
 __global__ void ens_gather_kernel(const float* __restrict__ bs, const float* __restrict__ ba,
                                   const float* __restrict__ bs2, const float* __restrict__ br, int64_t ptr,
                                   const int64_t* ptr_dev, int64_t cap, int64_t rows, const int64_t* idx,
-                                  uint64_t seed, uint64_t ctr, int S, int A, float* xs, float* xa, float* xt) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows) return;
+                                  uint64_t seed, uint64_t ctr, int S, int A, float* __restrict__ xs,
+                                  float* __restrict__ xa, float* __restrict__ xt) {
+  const int W = 2 * S + A + 1;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * W) return;
+  const int64_t i = e / W;
+  const int c = (int)(e - i * W);
   const int64_t p = ptr_dev ? *ptr_dev : ptr;
   const int64_t n = p < cap ? p : cap;
   int64_t j;
@@ -57,12 +66,15 @@ __global__ void ens_gather_kernel(const float* __restrict__ bs, const float* __r
     j = (int64_t)((((uint64_t)r.y << 32) | r.x) % (uint64_t)n);
   }
   const int64_t q = chrono_to_phys(j, p, cap);
-  for (int k = 0; k < S; ++k) {
-    xs[i * S + k] = bs[q * S + k];
-    xt[i * (S + 1) + k] = bs2[q * S + k];
+  if (c < S) {
+    xs[i * S + c] = bs[q * S + c];
+  } else if (c < S + A) {
+    xa[i * A + (c - S)] = ba[q * A + (c - S)];
+  } else if (c < 2 * S + A) {
+    xt[i * (S + 1) + (c - S - A)] = bs2[q * S + (c - S - A)];
+  } else {
+    xt[i * (S + 1) + S] = br[q];
   }
-  for (int k = 0; k < A; ++k) xa[i * A + k] = ba[q * A + k];
-  xt[i * (S + 1) + S] = br[q];
 }
 
 DRPO_API int drpo_ens_gather(const float* states, const float* actions, const float* next_states,
@@ -74,9 +86,10 @@ DRPO_API int drpo_ens_gather(const float* states, const float* actions, const fl
                "drpo_ens_gather: bad arguments");
   DRPO_REQUIRE(ptr_dev || ptr >= 1, "drpo_ens_gather: empty buffer");
   if (rows == 0) return DRPO_OK;
-  ens_gather_kernel<<<(unsigned)((rows + 255) / 256), 256, 0, stream>>>(states, actions, next_states, rewards, ptr,
-                                                                        ptr_dev, cap, rows, idx, seed, ctr, S, A,
-                                                                        xs, xa, xt);
+  const int64_t elems = rows * (2 * S + A + 1);
+  ens_gather_kernel<<<(unsigned)((elems + 255) / 256), 256, 0, stream>>>(states, actions, next_states, rewards, ptr,
+                                                                         ptr_dev, cap, rows, idx, seed, ctr, S, A,
+                                                                         xs, xa, xt);
   DRPO_LAUNCH_CHECK("ens_gather");
   return DRPO_OK;
 }
@@ -138,99 +151,150 @@ DRPO_API int drpo_ens_head(const float* D, const float* LVR, const float* s, int
 // ---------------------------------------------------------------------------
 // NLL loss + gradients
 // ---------------------------------------------------------------------------
-constexpr int LOSS_ROWS = 256;   // rows per block (split over blocks beyond that)
+// grid (row blocks of LOSS_ROWS, member). Thread t owns column k = t % KP of rows
+// r0 + t / KP, r0 + t / KP + 256 / KP, ... (KP = S1 rounded up to a power of two
+// >= 16), so the per-column log-var-bound gradients accumulate in registers. Each
+// block leaves its partial sums in the workspace; the last block to finish (ticket)
+// reduces them in a fixed order into the per-member NLL, the total loss and the
+// bound gradients -- one launch, no memset, deterministic sums.
+constexpr int LOSS_ROWS = 64;
 constexpr int LOSS_MAXS1 = 256;
 
-__global__ __launch_bounds__(256) void ens_loss_kernel(const float* D, const float* LVR, const float* s,
-                                                       int64_t s_zstride, const float* t, int64_t t_zstride, int64_t b,
-                                                       int S, const float* minlv, const float* maxlv,
-                                                       const float* gscale, float* mse, float* gD, float* gLVR,
-                                                       float* gmin, float* gmax) {
-  __shared__ float red[4];
-  __shared__ float cmin[LOSS_MAXS1], cmax[LOSS_MAXS1];
+struct LossWs {
+  int ticket;        // 0 between launches (the last block resets it)
+  int pad[63];
+  // followed by: float part_mse[Z * nbx], part_min[Z * nbx * S1], part_max[Z * nbx * S1]
+};
+
+__global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__ D, const float* __restrict__ LVR,
+                                                       const float* __restrict__ s, int64_t s_zstride,
+                                                       const float* __restrict__ t, int64_t t_zstride, int64_t b,
+                                                       int S, int Z, int KP, const float* __restrict__ minlv,
+                                                       const float* __restrict__ maxlv, float weight,
+                                                       const float* gscale, float* mse, float* loss, float* gD,
+                                                       float* gLVR, float* gmin, float* gmax, LossWs* ws) {
+  __shared__ float red[256];
+  __shared__ float rmin[256], rmax[256];
+  __shared__ int s_last;
   const int S1 = S + 1;
-  const int z = blockIdx.y;
+  const int nbx = gridDim.x;
+  const int z = blockIdx.y, bx = blockIdx.x;
   const int tid = threadIdx.x;
   const bool grads = gD != nullptr;
-  if (grads)
-    for (int k = tid; k < S1; k += 256) cmin[k] = cmax[k] = 0.f;
-  __syncthreads();
+  const int k = tid % KP, rl = tid / KP, RP = 256 / KP;
   const float inv_n = 1.f / (float)(b * S1);
   const float g = grads ? (gscale ? *gscale : 1.f) * inv_n : 0.f;
-  const int64_t r0 = (int64_t)blockIdx.x * LOSS_ROWS;
+  const int64_t r0 = (int64_t)bx * LOSS_ROWS;
   const int64_t r1 = min(b, r0 + LOSS_ROWS);
-  float sq = 0.f, ld = 0.f;
-  for (int64_t e = r0 * S1 + tid; e < r1 * S1; e += 256) {
-    const int64_t row = e / S1;
-    const int k = (int)(e - row * S1);
-    const int64_t o = (int64_t)z * b * S1 + e;
-    const float raw = LVR[o];
+  float acc = 0.f, cmin = 0.f, cmax = 0.f;
+  if (k < S1) {
     const float hi = maxlv[k], lo = minlv[k];
-    const float l1 = hi - softplusf(hi - raw);
-    const float l = lo + softplusf(l1 - lo);
-    const float m = D[o] + (k < S ? s[(int64_t)z * s_zstride + row * S + k] : 0.f);
-    const float diff = t[(int64_t)z * t_zstride + e] - m;
-    const float iv = expf(-l);
-    sq += diff * diff * iv;
-    ld += l;
-    if (grads) {
-      const float dl = (1.f - diff * diff * iv) * g;
-      const float s1 = sp_grad(l1 - lo), s2 = sp_grad(hi - raw);
-      gD[o] = -2.f * diff * iv * g;
-      gLVR[o] = dl * s1 * s2;
-      atomicAdd(&cmin[k], dl * (1.f - s1));
-      atomicAdd(&cmax[k], dl * s1 * (1.f - s2));
+    for (int64_t row = r0 + rl; row < r1; row += RP) {
+      const int64_t o = ((int64_t)z * b + row) * S1 + k;
+      const float raw = LVR[o];
+      const float l1 = hi - softplusf(hi - raw);
+      const float l = lo + softplusf(l1 - lo);
+      const float m = D[o] + (k < S ? s[(int64_t)z * s_zstride + row * S + k] : 0.f);
+      const float diff = t[(int64_t)z * t_zstride + row * S1 + k] - m;
+      const float iv = expf(-l);
+      acc += diff * diff * iv + l;
+      if (grads) {
+        const float dl = (1.f - diff * diff * iv) * g;
+        const float s1 = sp_grad(l1 - lo), s2 = sp_grad(hi - raw);
+        gD[o] = -2.f * diff * iv * g;
+        gLVR[o] = dl * s1 * s2;
+        cmin += dl * (1.f - s1);
+        cmax += dl * s1 * (1.f - s2);
+      }
     }
   }
-  // mean(sq) + mean(lv) for this member, accumulated over row blocks
-  float v = (sq + ld) * inv_n;
+  float* part_mse = reinterpret_cast<float*>(ws + 1);
+  float* part_min = part_mse + (size_t)Z * nbx;
+  float* part_max = part_min + (size_t)Z * nbx * S1;
+  // block partials: mean(sq) + mean(lv) contribution, per-column bound gradients
+  float v = acc * inv_n;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
   if ((tid & 63) == 0) red[tid >> 6] = v;
+  rmin[tid] = cmin;
+  rmax[tid] = cmax;
   __syncthreads();
-  if (tid == 0) atomicAdd(&mse[z], red[0] + red[1] + red[2] + red[3]);
-  if (grads)
-    for (int k = tid; k < S1; k += 256) {
-      atomicAdd(&gmin[k], cmin[k]);
-      atomicAdd(&gmax[k], cmax[k]);
+  const size_t pb = (size_t)z * nbx + bx;
+  if (tid == 0) part_mse[pb] = red[0] + red[1] + red[2] + red[3];
+  if (grads && tid < S1) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int q = 0; q < RP; ++q) {
+      a0 += rmin[q * KP + tid];
+      a1 += rmax[q * KP + tid];
     }
+    part_min[pb * S1 + tid] = a0;
+    part_max[pb * S1 + tid] = a1;
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&ws->ticket, 1) == nbx * Z - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  // last block: per-member NLL, total loss, bound gradients (fixed summation order)
+  const volatile float* pm = part_mse;
+  if (tid < Z) {
+    float m = 0.f;
+    for (int q = 0; q < nbx; ++q) m += pm[(size_t)tid * nbx + q];
+    mse[tid] = m;
+    red[tid] = m;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (loss) {
+      float tot = 0.f;
+      for (int zz = 0; zz < Z; ++zz) tot += red[zz];
+      float smax = 0.f, smin = 0.f;
+      for (int kk = 0; kk < S1; ++kk) {
+        smax += maxlv[kk];
+        smin += minlv[kk];
+      }
+      *loss = tot + weight * (smax - smin);
+    }
+    ws->ticket = 0;
+  }
+  if (grads && tid < S1) {
+    const volatile float* pn = part_min;
+    const volatile float* px = part_max;
+    float a0 = 0.f, a1 = 0.f;
+    for (size_t q = 0; q < (size_t)Z * nbx; ++q) {
+      a0 += pn[q * S1 + tid];
+      a1 += px[q * S1 + tid];
+    }
+    const float gw = (gscale ? *gscale : 1.f) * weight;
+    gmin[tid] += a0 - gw;
+    gmax[tid] += a1 + gw;
+  }
 }
 
-// loss = sum_z mse[z] + w * (sum(max) - sum(min)); d/dmax += w*g, d/dmin -= w*g
-__global__ void ens_loss_total_kernel(const float* mse, int Z, const float* minlv, const float* maxlv, int S1,
-                                      float weight, const float* gscale, float* loss, float* gmin, float* gmax) {
-  if (threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int z = 0; z < Z; ++z) tot += mse[z];
-    float smax = 0.f, smin = 0.f;
-    for (int k = 0; k < S1; ++k) {
-      smax += maxlv[k];
-      smin += minlv[k];
-    }
-    if (loss) *loss = tot + weight * (smax - smin);
-  }
-  if (gmin && (int)threadIdx.x < S1) {
-    const float g = (gscale ? *gscale : 1.f) * weight;
-    gmax[threadIdx.x] += g;
-    gmin[threadIdx.x] -= g;
-  }
+static int loss_kp(int S1) {
+  int kp = 16;
+  while (kp < S1) kp <<= 1;
+  return kp;
+}
+
+DRPO_API size_t drpo_ens_loss_workspace_size(int64_t b, int S, int Z) {
+  const size_t nbx = (size_t)((b + LOSS_ROWS - 1) / LOSS_ROWS);
+  return sizeof(LossWs) + sizeof(float) * (size_t)Z * nbx * (1 + 2 * (size_t)(S + 1));
 }
 
 DRPO_API int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
                            int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv,
                            float weight, const float* gscale, float* mse, float* loss, float* gD, float* gLVR,
-                           float* gmin, float* gmax, drpo_stream_t stream_) {
+                           float* gmin, float* gmax, void* workspace, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
-  DRPO_REQUIRE(D && LVR && s && t && minlv && maxlv && mse && b >= 1 && S >= 1 && S + 1 <= LOSS_MAXS1 && Z >= 1,
+  DRPO_REQUIRE(D && LVR && s && t && minlv && maxlv && mse && workspace && b >= 1 && S >= 1 &&
+                   S + 1 <= LOSS_MAXS1 && Z >= 1,
                "drpo_ens_loss: bad arguments");
   DRPO_REQUIRE(!gD == !gLVR && !gD == !gmin && !gD == !gmax, "drpo_ens_loss: gradient outputs all or none");
-  DRPO_CHECK_HIP(hipMemsetAsync(mse, 0, sizeof(float) * Z, stream));
+  DRPO_REQUIRE(Z <= 256, "drpo_ens_loss: at most 256 members");
   dim3 grid((unsigned)((b + LOSS_ROWS - 1) / LOSS_ROWS), Z);
-  ens_loss_kernel<<<grid, 256, 0, stream>>>(D, LVR, s, s_zstride, t, t_zstride, b, S, minlv, maxlv, gscale, mse, gD,
-                                            gLVR, gmin, gmax);
+  ens_loss_kernel<<<grid, 256, 0, stream>>>(D, LVR, s, s_zstride, t, t_zstride, b, S, Z, loss_kp(S + 1), minlv, maxlv,
+                                            weight, gscale, mse, loss, gD, gLVR, gmin, gmax, (LossWs*)workspace);
   DRPO_LAUNCH_CHECK("ens_loss");
-  if (loss || gmin) {
-    ens_loss_total_kernel<<<1, 256, 0, stream>>>(mse, Z, minlv, maxlv, S + 1, weight, gscale, loss, gmin, gmax);
-    DRPO_LAUNCH_CHECK("ens_loss_total");
-  }
   return DRPO_OK;
 }

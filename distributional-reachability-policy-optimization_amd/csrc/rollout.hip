@@ -751,7 +751,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     const int n_alive = __builtin_amdgcn_readfirstlane(*s_nalive);   // uniform exit
     if (n_alive == 0) {   // the whole tile finished: later steps see no rows from it
       for (int t2 = t + 1 + tid; t2 < p.H; t2 += NT) p.cnt[(size_t)t2 * p.ntiles + tile] = 0;
-      return;
+      break;
     }
   }
 }
@@ -793,6 +793,7 @@ __global__ __launch_bounds__(256) void rollout_scan_kernel(const int* __restrict
 template <int ROWS>
 __global__ __launch_bounds__(256) void rollout_emit_kernel(PersistArgs p, const int* __restrict__ pos,
                                                            const int* __restrict__ n, const int64_t* __restrict__ vptr,
+                                                           int advanced, const int64_t* __restrict__ offs,
                                                            int64_t vcap, float* __restrict__ vs, float* __restrict__ va,
                                                            float* __restrict__ vs2, float* __restrict__ vr,
                                                            float* __restrict__ vh, uint8_t* __restrict__ vd,
@@ -802,7 +803,8 @@ __global__ __launch_bounds__(256) void rollout_emit_kernel(PersistArgs p, const 
   if (tid == 0) {
     int64_t o = 0;
     for (int u = 0; u < t; ++u) o += n[u];
-    s_off = o + *vptr;
+    // rollout_scanfin_kernel already advanced the pointer by the total (offs[H])
+    s_off = o + *vptr - (advanced ? offs[p.H] : 0);
   }
   __syncthreads();
   const int slot = blockIdx.x * 256 + tid;
@@ -823,6 +825,51 @@ __global__ __launch_bounds__(256) void rollout_emit_kernel(PersistArgs p, const 
   const uint8_t dv = p.st_dv[src];
   vd[q] = dv & 1;
   vv[q] = (dv >> 1) & 1;
+}
+
+// Small rollouts (H x tiles <= 16384 counts): the per-step scans, the step offsets and
+// the pointer advance of rollout_scan_kernel + rollout_persist_finalize_kernel in ONE
+// single-workgroup launch (the emit then reads the advanced pointer minus the total).
+__global__ __launch_bounds__(256) void rollout_scanfin_kernel(const int* __restrict__ cnt, int* __restrict__ pos,
+                                                              int* __restrict__ n, int64_t* __restrict__ off,
+                                                              int64_t* __restrict__ vptr, int ntiles, int H) {
+  __shared__ int part[256];
+  __shared__ int s_tot;
+  const int tid = threadIdx.x;
+  int64_t total = 0;
+  for (int t = 0; t < H; ++t) {
+    const int* c = cnt + (size_t)t * ntiles;
+    int* ps = pos + (size_t)t * ntiles;
+    const int per = (ntiles + 255) / 256, b0 = tid * per;
+    int run = 0;
+    for (int i = 0; i < per; ++i)
+      if (b0 + i < ntiles) run += c[b0 + i];
+    part[tid] = run;
+    __syncthreads();
+    if (tid < 64) {
+      int v[4], sum = 0;
+      for (int q = 0; q < 4; ++q) { v[q] = part[tid * 4 + q]; sum += v[q]; }
+      int incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += y;
+      }
+      int e = incl - sum;
+      for (int q = 0; q < 4; ++q) { const int x = v[q]; part[tid * 4 + q] = e; e += x; }
+      if (tid == 63) { n[t] = incl; s_tot = incl; }
+    }
+    __syncthreads();
+    int e = part[tid];
+    for (int i = 0; i < per; ++i)
+      if (b0 + i < ntiles) { ps[b0 + i] = e; e += c[b0 + i]; }
+    if (tid == 0) off[t] = total;
+    total += s_tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    off[H] = total;
+    *vptr += total;
+  }
 }
 
 // off[t] = sum n[<t], off[H] = total; advance the buffer pointer
@@ -974,16 +1021,24 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
     rollout_persist_kernel<1, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   DRPO_LAUNCH_CHECK("rollout_persist");
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[1], stream);
-  rollout_scan_kernel<<<H, 256, 0, stream>>>(a.cnt, pos, n, a.ntiles);
-  DRPO_LAUNCH_CHECK("rollout_scan");
+  // small rollouts: scan + offsets + pointer advance in one single-workgroup launch
+  const int fin1 = (int64_t)H * a.ntiles <= 16384;
+  if (fin1) {
+    rollout_scanfin_kernel<<<1, 256, 0, stream>>>(a.cnt, pos, n, off, d->vptr, a.ntiles, H);
+    DRPO_LAUNCH_CHECK("rollout_scanfin");
+  } else {
+    rollout_scan_kernel<<<H, 256, 0, stream>>>(a.cnt, pos, n, a.ntiles);
+    DRPO_LAUNCH_CHECK("rollout_scan");
+  }
   const dim3 eg((unsigned)((a.ntiles * rpt + 255) / 256), (unsigned)H);
   if (rpt == 32)
-    rollout_emit_kernel<32><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, d->vcap, d->vs, d->va, d->vs2, d->vr, d->vh,
-                                                    d->vd, d->vv);
+    rollout_emit_kernel<32><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, fin1, off, d->vcap, d->vs, d->va,
+                                                    d->vs2, d->vr, d->vh, d->vd, d->vv);
   else
-    rollout_emit_kernel<16><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, d->vcap, d->vs, d->va, d->vs2, d->vr, d->vh,
-                                                    d->vd, d->vv);
+    rollout_emit_kernel<16><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, fin1, off, d->vcap, d->vs, d->va,
+                                                    d->vs2, d->vr, d->vh, d->vd, d->vv);
   DRPO_LAUNCH_CHECK("rollout_emit");
+  if (fin1) return DRPO_OK;
   rollout_persist_finalize_kernel<<<1, 1, 0, stream>>>(d->vptr, n, off, H);
   DRPO_LAUNCH_CHECK("rollout_finalize");
   return DRPO_OK;

@@ -84,10 +84,10 @@ class EnsembleEngine:
         return nets, strides
 
     # ------------------------------------------------------------------ forward
-    def _forward(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False, z0=0):
-        """Raw head outputs (D, LVR) [Z*n, S+1]; with save=True the activations needed
-        for the backward pass are kept (returns nets too)."""
-        m, L = self.m, _lib.lib()
+    def _forward_desc(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False, z0=0):
+        """Descriptor of one fused ensemble forward (raw head outputs D, LVR [Z*n, S+1]);
+        with save=True the activations needed for the backward pass are kept."""
+        m = self.m
         S, A = m.state_dim, m.action_dim
         S1 = S + 1
         m.group.ensure_packed()
@@ -107,7 +107,11 @@ class EnsembleEngine:
         norm = m.state_normalizer
         d = fill_fwd(nets, [(s, S), (a, A)], n, trunk=True, save_x=save_x, norm=(norm.mean, norm.std), nbatch=Z,
                      wstride=strides, sstride=[s_zs, a_zs, 0])
-        _lib.check(L.drpo_mlp_forward(ctypes.byref(d), _lib.stream()), 'ensemble forward')
+        return d, nets, strides, save_x
+
+    def _forward(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False, z0=0):
+        d, nets, strides, save_x = self._forward_desc(s, a, n, Z, s_zs, a_zs, member, tag, save, z0)
+        _lib.check(_lib.lib().drpo_mlp_forward(ctypes.byref(d), _lib.stream()), 'ensemble forward')
         return nets, strides, save_x
 
     def _head(self, D, LVR, s, s_zs, n, Zo, zsel=None, eps=None, noise=None, outputs=('mu', 'lv'), out=None):
@@ -183,8 +187,18 @@ class EnsembleEngine:
         return o['s2'], o['r']
 
     # ------------------------------------------------------------------ loss / grads
-    def _loss(self, nets, s, s_zs, t, t_zs, b, Z, grads, gscale=None, loss_out=None, tag='f', bound=True):
-        m, L = self.m, _lib.lib()
+    def _loss_ws(self, tag, b, Z):
+        """Zero-initialised workspace of drpo_ens_loss (its ticket resets itself)."""
+        nb = int(_lib.lib().drpo_ens_loss_workspace_size(b, self.m.state_dim, Z))
+        key = f'{tag}.lossws'
+        t = self.ws.get(key)
+        if t is None or t.numel() < nb:
+            t = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
+            self.ws[key] = t
+        return t
+
+    def _loss_args(self, nets, s, s_zs, t, t_zs, b, Z, grads, gscale=None, loss_out=None, tag='f', bound=True):
+        m = self.m
         S = m.state_dim
         S1 = S + 1
         g = m.group
@@ -194,17 +208,19 @@ class EnsembleEngine:
         if grads:
             gD, gL = self.buf(f'{tag}.gD', Z * b, S1), self.buf(f'{tag}.gL', Z * b, S1)
             gmin, gmax = g.view('min_log_var', g.grad), g.view('max_log_var', g.grad)
-        _lib.check(L.drpo_ens_loss(_lib.ptr(D), _lib.ptr(LVR), _lib.ptr(s), s_zs, _lib.ptr(t), t_zs, b, S, Z,
-                                   _lib.ptr(m.min_log_var), _lib.ptr(m.max_log_var),
-                                   float(m.log_var_bound_weight) if bound else 0.0,
-                                   _lib.ptr(gscale), _lib.ptr(mse), _lib.ptr(loss_out), _lib.ptr(gD), _lib.ptr(gL),
-                                   _lib.ptr(gmin), _lib.ptr(gmax), _lib.stream()), 'ens_loss')
+        args = [_lib.ptr(D), _lib.ptr(LVR), _lib.ptr(s), s_zs, _lib.ptr(t), t_zs, b, S, Z, _lib.ptr(m.min_log_var),
+                _lib.ptr(m.max_log_var), float(m.log_var_bound_weight) if bound else 0.0, _lib.ptr(gscale),
+                _lib.ptr(mse), _lib.ptr(loss_out), _lib.ptr(gD), _lib.ptr(gL), _lib.ptr(gmin), _lib.ptr(gmax),
+                _lib.ptr(self._loss_ws(tag, b, Z))]
+        return args, mse, gD, gL
+
+    def _loss(self, nets, s, s_zs, t, t_zs, b, Z, grads, gscale=None, loss_out=None, tag='f', bound=True):
+        args, mse, gD, gL = self._loss_args(nets, s, s_zs, t, t_zs, b, Z, grads, gscale, loss_out, tag, bound)
+        _lib.check(_lib.lib().drpo_ens_loss(*args, _lib.stream()), 'ens_loss')
         return mse, gD, gL
 
-    def _backward(self, nets, strides, save_x, gD, gL, b, Z):
-        L = _lib.lib()
+    def _backward_descs(self, nets, strides, save_x, gD, gL, b, Z):
         d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides)
-        _lib.check(L.drpo_mlp_backward(ctypes.byref(d), _lib.stream()), 'ensemble backward')
         items = []
         trunk_out = nets[0].sy[-1]
         for j, net in enumerate(nets):
@@ -216,8 +232,13 @@ class EnsembleEngine:
                 it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
                 it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
                 items.append(it)
-        arr = (WgradItem * len(items))(*items)
-        _lib.check(L.drpo_mlp_wgrad(arr, len(items), _lib.stream()), 'ensemble wgrad')
+        return d, (WgradItem * len(items))(*items), len(items)
+
+    def _backward(self, nets, strides, save_x, gD, gL, b, Z):
+        L = _lib.lib()
+        d, arr, n = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
+        _lib.check(L.drpo_mlp_backward(ctypes.byref(d), _lib.stream()), 'ensemble backward')
+        _lib.check(L.drpo_mlp_wgrad(arr, n, _lib.stream()), 'ensemble wgrad')
 
     def compute_loss_value(self, s, a, t, with_grads=False, gscale=None):
         """compute_loss on explicit rows (truncated to a multiple of E); returns a 0-d device
@@ -278,25 +299,53 @@ class EnsembleEngine:
         g = m.group
         g.grad.zero_()
         if sh is None:
-            segs = lambda sc: [m.optimizer.segment(0, g.size, sc, zero_grad=True, pack_map=g.pack_map())]  # noqa
+            segs = [m.optimizer.segment(0, g.size, (0.0, 1.0), zero_grad=True, pack_map=g.pack_map())]
         else:
             ranges = self._shard_ranges(z0, Z)
             lo, hi = g.offset('min_log_var'), g.offset('max_log_var') + S1
             bounds_grad = g.grad[lo:hi]
             pmap = g.pack_map()
-            segs = lambda sc: [m.optimizer.segment(a, c, sc, zero_grad=True, pack_map=pmap) for a, c in ranges]  # noqa
+            segs = [m.optimizer.segment(a, c, (0.0, 1.0), zero_grad=True, pack_map=pmap) for a, c in ranges]
+        # the whole step is built once (descriptors point at fixed workspaces); per step
+        # only the minibatch indices / Philox counter, the loss slot and Adam's bias-
+        # corrected step sizes change
+        from ._abi import OptimSeg
+        seg_arr = [(OptimSeg * len(segs[k:k + 8]))(*segs[k:k + 8]) for k in range(0, len(segs), 8)]
+        fd, nets, strides, save_x = self._forward_desc(xs, xa, b, Z, b * S, b * A, tag='fit', save=True, z0=z0)
+        largs, _, gD, gL = self._loss_args(nets, xs, b * S, xt, b * S1, b, Z, True, loss_out=losses[0:1], tag='fit',
+                                           bound=sh is None or sh.rank == 0)
+        bd, warr, nw = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
+        full = E * b if sh is not None else rows
+        idx_all = None
+        if nz.parity and steps > 0:
+            draws = [np.asarray(nz.randint(n, full))[z0 * b:z0 * b + rows] for _ in range(steps)]
+            idx_all = torch.from_numpy(np.ascontiguousarray(np.stack(draws), dtype=np.int64)).to(self.dev)
+        stream = _lib.stream()
+        gargs = [_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states), _lib.ptr(rb._rewards),
+                 ptr_host, _lib.ptr(ptr_dev), rb.capacity, rows]
+        gouts = [S, A, _lib.ptr(xs), _lib.ptr(xa), _lib.ptr(xt), stream]
+        loss_base = losses.data_ptr()
         for i in range(steps):
-            gather(rows, (xs, xa, xt), full=E * b if sh is not None else None)
-            nets, strides, save_x = self._forward(xs, xa, b, Z, b * S, b * A, tag='fit', save=True, z0=z0)
-            _, gD, gL = self._loss(nets, xs, b * S, xt, b * S1, b, Z, True, loss_out=losses[i], tag='fit',
-                                   bound=sh is None or sh.rank == 0)
-            self._backward(nets, strides, save_x, gD, gL, b, Z)
+            if idx_all is not None:
+                idx, ctr = ctypes.c_void_p(idx_all.data_ptr() + 8 * rows * i), 0
+            else:
+                idx, ctr = None, nz.next()
+            _lib.check(L.drpo_ens_gather(*gargs, idx, nz.seed, ctr, *gouts), 'ens_gather')
+            _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
+            largs[14] = ctypes.c_void_p(loss_base + 4 * i)
+            _lib.check(L.drpo_ens_loss(*largs, stream), 'ens_loss')
+            _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
+            _lib.check(L.drpo_mlp_wgrad(warr, nw, stream), 'ensemble wgrad')
             if sh is None:
                 self.dp.mean_(g.grad)
             else:
                 sh.sum_(bounds_grad)      # shared log-var bounds: the sum over all members
             # Adam + grad zeroing + packed-mirror refresh in one launch
-            fused_step(segs(m.optimizer.step_scalars()))
+            lr_bc1, bc2 = m.optimizer.step_scalars()
+            for arr in seg_arr:
+                for k in range(len(arr)):
+                    arr[k].lr_over_bc1, arr[k].bc2_sqrt = lr_bc1, bc2
+                _lib.check(L.drpo_optim_step(arr, len(arr), stream), 'optim_step')
         # holdout: the same rows for every member (src/dynamics.py:175-183)
         hb = m.holdout_size
         assert hb == b, 'reference asserts holdout_size == batch_size (src/dynamics.py:177)'

@@ -76,7 +76,7 @@ typedef struct {
   uint8_t *vd, *vv;
   int64_t* vptr;                 /* device int64 write pointer, advanced by the rollout */
   int64_t vcap;
-  void* workspace;               /* drpo_rollout_workspace_size bytes */
+  void* workspace;               /* drpo_rollout_workspace_size bytes; one rollout at a time per workspace */
   int rows_per_tile;             /* 16 or 32, 0 = auto */
   void** step_events;            /* optional [2*H] events: engine 1 records pair t around step t's kernel,
                                     engine 2 records pair 0 around the fused horizon kernel */
@@ -311,11 +311,16 @@ int drpo_ens_head(const float* D, const float* LVR, const float* s, int64_t s_zs
                   const float* minlv, const float* maxlv, const int* zsel, const float* eps, uint64_t seed,
                   uint64_t ctr, float* mu, float* lv, float* s2, float* r, drpo_stream_t stream);
 /* per-member NLL (_mse_loss, src/dynamics.py:236-253), total compute_loss (:143-153)
- * and, when gD != NULL, its gradients (scaled by *gscale if given) */
+ * and, when gD != NULL, its gradients (scaled by *gscale if given; gmin/gmax are
+ * accumulated into). One launch: the last block reduces the per-block partials.
+ * workspace: drpo_ens_loss_workspace_size(b, S, Z) bytes, ZERO-initialised once by
+ * the caller (its leading counter returns to zero after every call); one call at a
+ * time per workspace. */
+size_t drpo_ens_loss_workspace_size(int64_t b, int S, int Z);
 int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
                   int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv, float weight,
                   const float* gscale, float* mse, float* loss, float* gD, float* gLVR, float* gmin, float* gmax,
-                  drpo_stream_t stream);
+                  void* workspace, drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam (coupled L2), clip_grad_norm_, update_ema (src/ssac.py:446-455,
