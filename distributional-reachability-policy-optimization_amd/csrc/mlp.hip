@@ -417,37 +417,63 @@ __device__ __forceinline__ float act_grad(int act, float y, float z) {
   }
 }
 
+// The one saved value act_grad reads for layer L (post-activation y for relu / tanh,
+// pre-activation z for swish), 8 elements per thread of the tile's [16][wpad] grid,
+// loaded into registers one layer AHEAD: issued before the previous layer's
+// backward GEMM, they arrive while it runs instead of stalling the elementwise phase.
+constexpr int BW_PER = FW_ROWS * 256 / FW_NT;   // 8 elements per thread (widths <= 256)
+
+__device__ __forceinline__ void bwd_fetch_act(const drpo_mlp_bwd_layer_t& __restrict__ L, int z, int64_t rows,
+                                              int row0, int nrows, float (&v)[BW_PER]) {
+  const int tid = threadIdx.x;
+  const int dout = L.dout, act = L.act;
+  const float* __restrict__ src = act == ACT_SILU ? L.sz : L.sy;
+  const size_t so = ((size_t)z * rows + row0) * dout;
+  const int wpad = round_up(dout, 16);
+#pragma unroll
+  for (int i = 0; i < BW_PER; ++i) {
+    const int e = tid + i * FW_NT;
+    const int r = e / wpad, k = e - r * wpad;
+    v[i] = (act != ACT_NONE && src && e < FW_ROWS * wpad && r < nrows && k < dout)
+               ? gload(src + so + (size_t)r * dout + k) : 0.f;
+  }
+}
+
+__device__ __forceinline__ float act_grad_saved(int act, float saved) {
+  return act == ACT_SILU ? act_grad(act, 0.f, saved) : act_grad(act, saved, 0.f);
+}
+
 // G (LDS, width of the net output) -> gradient w.r.t. the net input (returned LDS buffer)
 __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__ net, float* G, float* bA, float* bB, int z, int64_t rows,
                           int row0, int nrows, bool need_dx0) {
   const int tid = threadIdx.x;
   float* cur = G;
+  float sv[BW_PER];
+  bwd_fetch_act(net.L[net.nl - 1], z, rows, row0, nrows, sv);
   for (int l = net.nl - 1; l >= 0; --l) {
     const drpo_mlp_bwd_layer_t& L = net.L[l];
     // descriptor fields into registers once per layer (no reloads inside the loops)
     const int dout = L.dout, din = L.din, act = L.act;
-    const float* __restrict__ sy = L.sy;
-    const float* __restrict__ sz = L.sz;
     float* __restrict__ dzp = L.dz;
     const float* W = L.W + (size_t)z * L.wstride;
     const size_t so = ((size_t)z * rows + row0) * dout;
     const int wpad = round_up(dout, 16);
-#pragma unroll 8
-    for (int e = tid; e < FW_ROWS * wpad; e += FW_NT) {
+#pragma unroll
+    for (int i = 0; i < BW_PER; ++i) {
+      const int e = tid + i * FW_NT;
+      if (e >= FW_ROWS * wpad) break;
       const int r = e / wpad, k = e - r * wpad;
       float g = 0.f;
       if (r < nrows && k < dout) {
         g = cur[r * LDH + k];
-        if (act != ACT_NONE) {
-          const size_t idx = so + (size_t)r * dout + k;
-          g *= act_grad(act, sy ? gload(sy + idx) : 0.f, sz ? gload(sz + idx) : 0.f);
-        }
+        if (act != ACT_NONE) g *= act_grad_saved(act, sv[i]);
         if (dzp) gstore(dzp + so + (size_t)r * dout + k, g);
       }
       cur[r * LDH + k] = g;
     }
     lds_barrier();
     if (l == 0 && !need_dx0) return nullptr;   // input gradient not wanted: dZ_0 (saved) is all wgrad needs
+    if (l > 0) bwd_fetch_act(net.L[l - 1], z, rows, row0, nrows, sv);   // next layer's, during this GEMM
     float* out = (cur == bA) ? bB : bA;
     // dY_prev = dZ W: transposed mirror, N = din, K = dout
     tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, dout, W, nullptr, din, out, LDH);

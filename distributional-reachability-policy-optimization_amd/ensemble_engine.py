@@ -188,7 +188,7 @@ class EnsembleEngine:
 
     # ------------------------------------------------------------------ loss / grads
     def _loss_ws(self, tag, b, Z):
-        """Zero-initialised workspace of drpo_ens_loss (its ticket resets itself)."""
+        """Partial-sum workspace of drpo_ens_loss."""
         nb = int(_lib.lib().drpo_ens_loss_workspace_size(b, self.m.state_dim, Z))
         key = f'{tag}.lossws'
         t = self.ws.get(key)

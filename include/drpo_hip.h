@@ -312,10 +312,9 @@ int drpo_ens_head(const float* D, const float* LVR, const float* s, int64_t s_zs
                   uint64_t ctr, float* mu, float* lv, float* s2, float* r, drpo_stream_t stream);
 /* per-member NLL (_mse_loss, src/dynamics.py:236-253), total compute_loss (:143-153)
  * and, when gD != NULL, its gradients (scaled by *gscale if given; gmin/gmax are
- * accumulated into). One launch: the last block reduces the per-block partials.
- * workspace: drpo_ens_loss_workspace_size(b, S, Z) bytes, ZERO-initialised once by
- * the caller (its leading counter returns to zero after every call); one call at a
- * time per workspace. */
+ * accumulated into). Row blocks leave partial sums in the workspace
+ * (drpo_ens_loss_workspace_size(b, S, Z) bytes; one call at a time per workspace),
+ * reduced in a fixed order by a one-block launch. */
 size_t drpo_ens_loss_workspace_size(int64_t b, int S, int Z);
 int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
                   int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv, float weight,
