@@ -12,3 +12,7 @@ from .ssac import SSAC, CriticEnsemble, ConstraintCritic, MLPMultiplier  # noqa:
 from .smbpo import SMBPO  # noqa: F401
 from .rng import DeviceNoise, TapeNoise  # noqa: F401
 from .torch_util import set_seed, device  # noqa: F401
+from .policy import UniformPolicy  # noqa: F401,E402
+from .checkpoint import CheckpointableData, Checkpointer  # noqa: F401,E402
+from .envs import ProductEnv  # noqa: F401,E402
+from .sampling import sample_episodes_batched  # noqa: F401,E402
