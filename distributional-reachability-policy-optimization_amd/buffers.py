@@ -12,6 +12,21 @@ import torch.nn as nn
 from .torch_util import device as default_device
 
 
+def sample_without_replacement(high, size, device):
+    """``random_indices(high, size, replace=False)`` (src/torch_util.py:41-44) on the
+    device: a keyed pseudo-random permutation evaluated at 0..size-1
+    (drpo_sample_without_replacement). The key comes from torch's host generator,
+    so ``torch.manual_seed`` makes it reproducible; no host<->device sync."""
+    from . import _lib
+    if not 0 <= size <= high:
+        raise ValueError(f'cannot take {size} distinct indices out of {high}')
+    idx = torch.empty(size, dtype=torch.int64, device=device)
+    seed, ctr = (int(v) for v in torch.randint(0, 2 ** 62, (2,)))
+    _lib.check(_lib.lib().drpo_sample_without_replacement(_lib.ptr(idx), size, high, seed, ctr, _lib.stream()),
+               'sample_without_replacement')
+    return idx
+
+
 class SampleBuffer(nn.Module):
     COMPONENT_NAMES = ('states', 'actions', 'next_states', 'rewards', 'dones')
 
@@ -118,8 +133,10 @@ class SampleBuffer(nn.Module):
         self._set_pointer(p + n)
 
     def sample(self, batch_size, replace=True, device=default_device, include_indices=False):
-        assert replace, 'sampling without replacement is not on the hot path'
-        idx = torch.randint(len(self), [batch_size], device=self.device)
+        if replace:
+            idx = torch.randint(len(self), [batch_size], device=self.device)
+        else:
+            idx = sample_without_replacement(len(self), batch_size, self.device)
         bufs = [self._bufs[n][idx].to(device) for n in self.COMPONENT_NAMES]
         return (bufs, idx) if include_indices else bufs
 

@@ -1,5 +1,8 @@
 """Build libdrpo_hip.so (gfx950) in-tree: hipcc each csrc/*.hip to an object, link a
-shared library. Incremental (skips objects newer than their sources/headers)."""
+shared library. Incremental by content: an object is rebuilt unless the SHA-256 of
+(compiler version, flags, its source, every header) matches the digest stored next
+to it, so copied trees with shuffled mtimes still rebuild exactly what changed."""
+import hashlib
 import glob
 import os
 import subprocess
@@ -15,65 +18,94 @@ FLAGS = ['-O3', '--offload-arch=gfx950', '-std=c++17', '-fPIC', '-Wall', '-Wno-u
          '-Wno-unused-variable', '-Wno-unused-but-set-variable', '-fvisibility=hidden']
 
 
-def _stale(src, obj, headers):
-    if not os.path.exists(obj):
+_CC_VERSION = None
+
+
+def _cc_version():
+    global _CC_VERSION
+    if _CC_VERSION is None:
+        r = subprocess.run([HIPCC, '--version'], capture_output=True, text=True)
+        _CC_VERSION = r.stdout if r.returncode == 0 else HIPCC
+    return _CC_VERSION
+
+
+def _digest(src, headers, flags):
+    h = hashlib.sha256()
+    h.update(_cc_version().encode())
+    h.update('\0'.join(flags).encode())
+    for p in [src] + sorted(headers):
+        h.update(os.path.basename(p).encode())
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stale(obj, digest):
+    try:
+        with open(obj + '.sha256') as f:
+            return f.read().strip() != digest or not os.path.exists(obj)
+    except OSError:
         return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(p) > t for p in [src] + headers)
+
+
+def _compile(src, obj, flags, digest, verbose=False):
+    cmd = [HIPCC] + flags + ['-I', os.path.join(HERE, '..', 'include'), '-c', src, '-o', obj]
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')
+    with open(obj + '.sha256', 'w') as f:
+        f.write(digest)
+    return obj
+
+
+def _link(objs, lib, force):
+    """Relink when an object changed or the library's recorded object digests differ."""
+    key = hashlib.sha256()
+    for o in objs:
+        with open(o + '.sha256') as f:
+            key.update(f.read().encode())
+    key = key.hexdigest()
+    if not force and os.path.exists(lib):
+        try:
+            with open(lib + '.sha256') as f:
+                if f.read().strip() == key:
+                    return lib
+        except OSError:
+            pass
+    r = subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', lib] + objs, capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'link failed:\n{r.stderr}')
+    with open(lib + '.sha256', 'w') as f:
+        f.write(key)
+    return lib
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, '*.hpp')) + glob.glob(os.path.join(HERE, '..', 'include', '*.h'))
+
+
+def _build(flags, lib, objdir, verbose, jobs):
+    os.makedirs(objdir, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    headers = _headers()
+    objs = [os.path.join(objdir, os.path.basename(s)[:-4] + '.o') for s in srcs]
+    digs = [_digest(s, headers, flags) for s in srcs]
+    todo = [(s, o, d) for s, o, d in zip(srcs, objs, digs) if _stale(o, d)]
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(lambda t: _compile(t[0], t[1], flags, t[2], verbose), todo))
+    return _link(objs, lib, force=bool(todo))
 
 
 def build(verbose=False, jobs=8, variant=None):
     """variant='stamps': profiling build with in-kernel s_memtime stamps (-DDRPO_STAMPS)
     into libdrpo_hip_stamps.so; never loaded by the product."""
     if variant == 'stamps':
-        return _build_variant(['-DDRPO_STAMPS'], os.path.join(HERE, 'libdrpo_hip_stamps.so'), 'build_stamps', verbose,
-                              jobs)
-    os.makedirs(OBJ, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
-    headers = glob.glob(os.path.join(CSRC, '*.hpp')) + glob.glob(os.path.join(HERE, '..', 'include', '*.h'))
-    objs = [os.path.join(OBJ, os.path.basename(s)[:-4] + '.o') for s in srcs]
-    todo = [(s, o) for s, o in zip(srcs, objs) if _stale(s, o, headers)]
-
-    def cc(so):
-        s, o = so
-        cmd = [HIPCC] + FLAGS + ['-I', os.path.join(HERE, '..', 'include'), '-c', s, '-o', o]
-        if verbose:
-            print(' '.join(cmd), flush=True)
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f'hipcc failed for {s}:\n{r.stderr}')
-        return o
-
-    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        list(ex.map(cc, todo))
-    if todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', LIB] + objs
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f'link failed:\n{r.stderr}')
-    return LIB
-
-
-def _build_variant(defs, lib, objdir, verbose, jobs):
-    od = os.path.join(HERE, objdir)
-    os.makedirs(od, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
-    objs = [os.path.join(od, os.path.basename(s)[:-4] + '.o') for s in srcs]
-
-    def cc(so):
-        s, o = so
-        cmd = [HIPCC] + FLAGS + defs + ['-I', os.path.join(HERE, '..', 'include'), '-c', s, '-o', o]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f'hipcc failed for {s}:\n{r.stderr}')
-
-    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        list(ex.map(cc, zip(srcs, objs)))
-    r = subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', lib] + objs, capture_output=True,
-                       text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f'link failed:\n{r.stderr}')
-    return lib
+        return _build(FLAGS + ['-DDRPO_STAMPS'], os.path.join(HERE, 'libdrpo_hip_stamps.so'),
+                      os.path.join(HERE, 'build_stamps'), verbose, jobs)
+    return _build(FLAGS, LIB, OBJ, verbose, jobs)
 
 
 if __name__ == '__main__':

@@ -191,3 +191,66 @@ def test_rollout_production_mode_runs_and_conserves_rows():
     # a row continues iff it was not done: count of step-(t+1) rows == alive rows at step t
     assert torch.isfinite(got['next_states']).all()
     assert (got['actions'].abs() <= 1).all()
+
+
+def _prod_alg(seed):
+    cfg = drpo_amd.SMBPO.Config()
+    cfg.update({'horizon': 5, 'rollout_batch_size': 2048, 'buffer_max': 50000})
+    torch.manual_seed(3)
+    alg = drpo_amd.SMBPO(cfg, lambda id=None: ENVS['quadrotor'](), None, 1, device=DEV, noise_seed=seed)
+    N = 8000
+    g = torch.Generator(device='cpu').manual_seed(11)
+    s = torch.randn(N, 12, generator=g).to(DEV)
+    s[:, 2] = s[:, 2].abs() * 0.2 + 0.6
+    z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=DEV)
+    alg.replay_buffer.extend(states=s, actions=z(N, 2), next_states=s, rewards=z(N), dones=z(N, dt=torch.bool),
+                             violations=z(N, dt=torch.bool), constraint_values=z(N, 2))
+    alg.model_ensemble.state_normalizer.fit(s)
+    alg.model_ensemble._elite_inds = [0, 1, 2, 3, 4]
+    return alg
+
+
+def test_device_noise_seed_controls_rollout_draws():
+    """the production noise key follows the seed -- the same seed (on fresh,
+    identically initialised trainers) reproduces the rollout bit for bit, another seed
+    draws different initial states and noise."""
+    a1, a2, b = _prod_alg(101), _prod_alg(101), _prod_alg(202)
+    r1, r2, r3 = (x.rollout(x.actor).get(as_dict=True) for x in (a1, a2, b))
+    for k in COMP:
+        assert torch.equal(r1[k], r2[k]), k
+    assert not torch.equal(r1['states'][:2048], r3['states'][:2048])
+    assert not torch.equal(r1['actions'][:2048], r3['actions'][:2048])
+
+
+@pytest.mark.parametrize('high,size', [(10, 10), (1000, 37), (100000, 4096), (5, 0)])
+def test_buffer_sample_without_replacement(high, size):
+    """SampleBuffer.sample(replace=False) (src/sampling.py:147-151): distinct in-range rows."""
+    from drpo_amd.buffers import SampleBuffer
+    buf = SampleBuffer(3, 2, high, device=DEV)
+    st = torch.arange(high, dtype=torch.float32, device=DEV)[:, None].repeat(1, 3)
+    z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=DEV)
+    buf.extend(states=st, actions=z(high, 2), next_states=st, rewards=z(high), dones=z(high, dt=torch.bool))
+    (s, *_), idx = buf.sample(size, replace=False, device=DEV, include_indices=True)
+    assert idx.shape == (size,) and torch.unique(idx).numel() == size
+    if size:
+        assert int(idx.min()) >= 0 and int(idx.max()) < high
+    assert torch.equal(s[:, 0].long(), idx)
+    with pytest.raises(ValueError):
+        buf.sample(high + 1, replace=False, device=DEV)
+
+
+def test_cartpole_threshold_follows_env():
+    """the cartpole constraint uses the env's own threshold
+    (src/env/poles/inverted_pendulum.py:11-17), not the default 0.2."""
+    from drpo_amd import envs, ops
+
+    class SafeInvertedPendulumEnv:
+        x_threshold, th_threshold = 0.9, 0.35
+    p = envs.device_env_params(SafeInvertedPendulumEnv())
+    assert p['env_id'] == 2 and p['thr1'] == 0.35
+    s = torch.randn(513, 4, device=DEV)
+    done, viol, h = ops.env_constraints(p, s)
+    x, t = s[:, 0].double(), s[:, 1].double()
+    ref = torch.stack([-x - 0.9, -t - 0.35, x - 0.9, t - 0.35], 1)
+    assert torch.equal(h, ref.float())
+    assert torch.equal(viol, (ref > 0).any(1)) and torch.equal(done, viol)
