@@ -115,13 +115,13 @@ class MlpFwd(ctypes.Structure):
     """drpo_mlp_fwd_t"""
     _fields_ = [('src', P * 3), ('cols', c_int * 3), ('ld', c_int * 3), ('sstride', c_int64 * 3),
                 ('nmean', P), ('nstd', P), ('save_x', P), ('net', MlpNet * 3), ('nnets', c_int), ('trunk', c_int),
-                ('rows', c_int64), ('nbatch', c_int), ('head', PolicyHead)]
+                ('rows', c_int64), ('nbatch', c_int), ('head', PolicyHead), ('split_heads', c_int)]
 
 
 class MlpBwdLayer(ctypes.Structure):
     """drpo_mlp_bwd_layer_t"""
     _fields_ = [('W', P), ('din', c_int), ('dout', c_int), ('act', c_int), ('sy', P), ('sz', P), ('dz', P),
-                ('wstride', c_int64)]
+                ('wstride', c_int64), ('dz2', P)]
 
 
 class MlpBwdNet(ctypes.Structure):
@@ -131,7 +131,8 @@ class MlpBwdNet(ctypes.Structure):
 
 class MlpBwd(ctypes.Structure):
     """drpo_mlp_bwd_t"""
-    _fields_ = [('net', MlpBwdNet * 3), ('nnets', c_int), ('trunk', c_int), ('rows', c_int64), ('nbatch', c_int)]
+    _fields_ = [('net', MlpBwdNet * 3), ('nnets', c_int), ('trunk', c_int), ('rows', c_int64), ('nbatch', c_int),
+                ('split_heads', c_int)]
 
 
 class WgradItem(ctypes.Structure):

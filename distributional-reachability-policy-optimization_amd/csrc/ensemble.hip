@@ -151,15 +151,15 @@ DRPO_API int drpo_ens_head(const float* D, const float* LVR, const float* s, int
 // ---------------------------------------------------------------------------
 // NLL loss + gradients
 // ---------------------------------------------------------------------------
-// grid (row blocks of LOSS_ROWS, member). Thread t owns column k = t % KP of rows
-// r0 + t / KP, r0 + t / KP + 256 / KP, ... (KP = S1 rounded up to a power of two
-// >= 16), so the per-column log-var-bound gradients accumulate in registers. Each
+// grid (row blocks of 256 / KP rows, member). Thread t owns column k = t % KP of row
+// r0 + t / KP (KP = S1 rounded up to a power of two >= 16): one row per thread, so a
+// block waits one memory latency (64-row blocks looped 4 times: 9.2 us per launch at
+// E=7, b=256; the per-column log-var-bound partials are reduced through LDS). Each
 // block leaves its partial sums in the workspace and ens_loss_reduce_kernel (one
 // block) sums them in a fixed order into the per-member NLL, the total loss and the
 // bound gradients: deterministic, no memset, and no in-kernel cross-workgroup hand-
 // off (a device-scope fence writes back the whole XCD L2 on gfx950: measured 22 us
 // for a last-block variant of this kernel).
-constexpr int LOSS_ROWS = 64;
 constexpr int LOSS_MAXS1 = 256;
 
 __global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__ D, const float* __restrict__ LVR,
@@ -178,8 +178,8 @@ __global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__
   const int k = tid % KP, rl = tid / KP, RP = 256 / KP;
   const float inv_n = 1.f / (float)(b * S1);
   const float g = grads ? (gscale ? *gscale : 1.f) * inv_n : 0.f;
-  const int64_t r0 = (int64_t)bx * LOSS_ROWS;
-  const int64_t r1 = min(b, r0 + LOSS_ROWS);
+  const int64_t r0 = (int64_t)bx * RP;     // one row per thread (launcher: 256 / KP rows)
+  const int64_t r1 = min(b, r0 + RP);
   float acc = 0.f, cmin = 0.f, cmax = 0.f;
   if (k < S1) {
     const float hi = maxlv[k], lo = minlv[k];
@@ -224,22 +224,54 @@ __global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__
   }
 }
 
-// per-member NLL, total loss, bound gradients from the block partials (fixed order)
+// per-member NLL, total loss, bound gradients from the block partials. Every sum is
+// spread over 16 lanes (strided partials, then a fixed xor tree), so the kernel waits
+// a couple of memory latencies instead of one per partial; the order is fixed, so the
+// result is deterministic.
 __global__ __launch_bounds__(256) void ens_loss_reduce_kernel(const float* __restrict__ part, int nbx, int Z, int S1,
                                                               const float* __restrict__ minlv,
                                                               const float* __restrict__ maxlv, float weight,
                                                               const float* gscale, float* mse, float* loss,
                                                               float* gmin, float* gmax) {
-  __shared__ float red[256];
+  __shared__ float red[256], smx[LOSS_MAXS1], smn[LOSS_MAXS1];
   const int tid = threadIdx.x;
+  const int grp = tid >> 4, l16 = tid & 15;
   const float* part_mse = part;
   const float* part_min = part_mse + (size_t)Z * nbx;
   const float* part_max = part_min + (size_t)Z * nbx * S1;
-  if (tid < Z) {
+  for (int z = grp; z < Z; z += 16) {
     float m = 0.f;
-    for (int q = 0; q < nbx; ++q) m += part_mse[(size_t)tid * nbx + q];
-    mse[tid] = m;
-    red[tid] = m;
+    for (int q = l16; q < nbx; q += 16) m += part_mse[(size_t)z * nbx + q];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) m += __shfl_xor(m, o, 16);
+    if (l16 == 0) {
+      mse[z] = m;
+      red[z] = m;
+    }
+  }
+  const size_t Q = (size_t)Z * nbx;
+  const float gw = gmin ? (gscale ? *gscale : 1.f) * weight : 0.f;
+  for (int c = grp; c < S1; c += 16) {
+    if (gmin) {
+      float a0 = 0.f, a1 = 0.f;
+      for (size_t q = l16; q < Q; q += 16) {
+        a0 += part_min[q * S1 + c];
+        a1 += part_max[q * S1 + c];
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        a0 += __shfl_xor(a0, o, 16);
+        a1 += __shfl_xor(a1, o, 16);
+      }
+      if (l16 == 0) {
+        gmin[c] += a0 - gw;
+        gmax[c] += a1 + gw;
+      }
+    }
+    if (l16 == 0) {
+      smx[c] = maxlv[c];
+      smn[c] = minlv[c];
+    }
   }
   __syncthreads();
   if (tid == 0 && loss) {
@@ -247,22 +279,15 @@ __global__ __launch_bounds__(256) void ens_loss_reduce_kernel(const float* __res
     for (int zz = 0; zz < Z; ++zz) tot += red[zz];
     float smax = 0.f, smin = 0.f;
     for (int kk = 0; kk < S1; ++kk) {
-      smax += maxlv[kk];
-      smin += minlv[kk];
+      smax += smx[kk];
+      smin += smn[kk];
     }
     *loss = tot + weight * (smax - smin);
   }
-  if (gmin && tid < S1) {
-    float a0 = 0.f, a1 = 0.f;
-    for (size_t q = 0; q < (size_t)Z * nbx; ++q) {
-      a0 += part_min[q * S1 + tid];
-      a1 += part_max[q * S1 + tid];
-    }
-    const float gw = (gscale ? *gscale : 1.f) * weight;
-    gmin[tid] += a0 - gw;
-    gmax[tid] += a1 + gw;
-  }
 }
+
+// rows per loss workgroup: one row per thread (256 / KP rows of KP column lanes)
+static int loss_rows(int S1);
 
 static int loss_kp(int S1) {
   int kp = 16;
@@ -270,8 +295,11 @@ static int loss_kp(int S1) {
   return kp;
 }
 
+static int loss_rows(int S1) { return 256 / loss_kp(S1); }
+
 DRPO_API size_t drpo_ens_loss_workspace_size(int64_t b, int S, int Z) {
-  const size_t nbx = (size_t)((b + LOSS_ROWS - 1) / LOSS_ROWS);
+  const int rows = loss_rows(S + 1);
+  const size_t nbx = (size_t)((b + rows - 1) / rows);
   return sizeof(float) * (size_t)Z * nbx * (1 + 2 * (size_t)(S + 1));
 }
 
@@ -285,7 +313,10 @@ DRPO_API int drpo_ens_loss(const float* D, const float* LVR, const float* s, int
                "drpo_ens_loss: bad arguments");
   DRPO_REQUIRE(!gD == !gLVR && !gD == !gmin && !gD == !gmax, "drpo_ens_loss: gradient outputs all or none");
   DRPO_REQUIRE(Z <= 256, "drpo_ens_loss: at most 256 members");
-  const int nbx = (int)((b + LOSS_ROWS - 1) / LOSS_ROWS);
+  const int rows = loss_rows(S + 1);
+  const int64_t nbx64 = (b + rows - 1) / rows;
+  DRPO_REQUIRE(nbx64 <= (1 << 30), "drpo_ens_loss: too many rows");
+  const int nbx = (int)nbx64;
   ens_loss_kernel<<<dim3((unsigned)nbx, Z), 256, 0, stream>>>(D, LVR, s, s_zstride, t, t_zstride, b, S, Z,
                                                              loss_kp(S + 1), minlv, maxlv, gscale, gD, gLVR,
                                                              (float*)workspace);

@@ -50,9 +50,21 @@ __device__ unsigned long long g_stamps[1 << 16][16];
 DRPO_API int drpo_debug_stamps(unsigned long long* dst, int n) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * (size_t)n);
 }
+// wgrad stamps: rows 32768.. of the same buffer (the forward's slots stay intact)
+#define STAMPW(i)                                                                                 \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long _t;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 32768u) g_stamps[32768 + blockIdx.x][(i)] = _t;          \
+  } while (0)
 #else
 #define STAMP(i) \
   do {           \
+  } while (0)
+#define STAMPW(i) \
+  do {            \
   } while (0)
 #endif
 template <int ACT, int RB>
@@ -68,11 +80,11 @@ __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const dr
 // optional global saves of the post-/pre-activation for the backward pass
 template <int RB = 1>
 __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& __restrict__ L, int z, int64_t rows,
-                                          int row0, int nrows, float* out, float* red) {
+                                          int row0, int nrows, float* out, float* red, bool save = true) {
   const float* W = L.W + (size_t)z * L.wstride;
   const float* b = L.b + (size_t)z * L.bstride;
   const size_t so = ((size_t)z * rows + row0) * L.dout;
-  GSave gs{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
+  GSave gs{save && L.sy ? L.sy + so : nullptr, save && L.sz ? L.sz + so : nullptr, L.dout, nrows};
   switch (L.act) {
     case ACT_RELU: run_layer_act<ACT_RELU, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
     case ACT_SILU: run_layer_act<ACT_SILU, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
@@ -87,13 +99,13 @@ __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_m
 // buffer holding the final activation.
 template <int NI>
 __device__ __forceinline__ float* run_net(const drpo_mlp_fwd_t& a, float* in, float* bufA, float* bufB, int z, int row0, int nrows,
-                          float* red) {
+                          float* red, bool save = true) {
   float* cur = in;
 #pragma unroll
   for (int l = 0; l < MAXL; ++l) {
     if (l < a.net[NI].nl) {
       float* out = (cur == bufA) ? bufB : bufA;
-      run_layer(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red);
+      run_layer(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red, save);
       lds_barrier();
       STAMP(2 + 4 * NI + l);
       cur = out;
@@ -110,12 +122,17 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
   float* T = bB + FW_ROWS * LDH;           // trunk output (trunk mode)
   float* red = T + FW_ROWS * LDH;          // FW_NW * 256
   const int tid = threadIdx.x;
-  const int z = blockIdx.z;
-  const int row0 = blockIdx.x * FW_ROWS;
+  const LogicalBlock lb = xcd_block();   // one member's tiles per XCD (shared weights in L2)
+  const int z = lb.z;
+  const int row0 = lb.x * FW_ROWS;
   if (row0 >= a.rows) return;
   const int nrows = (int)min((int64_t)FW_ROWS, a.rows - row0);
   const int din0 = a.cols[0] + a.cols[1] + a.cols[2];
   const int kpad = round_up(din0, 16);
+  // split heads: this workgroup runs the trunk and head lb.y + 1; only head 1's
+  // workgroup writes the trunk-side saves
+  const bool split = a.trunk && a.split_heads;
+  const bool tsave = !split || lb.y == 0;
   STAMP(0);
 
   for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
@@ -136,16 +153,21 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
       }
       v = src[kk];
       if (k < a.cols[0] && a.nmean) v = (v - a.nmean[kk]) / (a.nstd[kk] + 1e-6f);
-      if (a.save_x) a.save_x[((size_t)z * a.rows + row) * din0 + k] = v;
+      if (a.save_x && tsave) a.save_x[((size_t)z * a.rows + row) * din0 + k] = v;
     }
     xin[r * LDH + k] = v;
   }
   lds_barrier();
   STAMP(1);
   if (!a.trunk) {
-    if (blockIdx.y == 0) run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
-    else if (blockIdx.y == 1) run_net<1>(a, xin, bA, bB, z, row0, nrows, red);
+    if (lb.y == 0) run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
+    else if (lb.y == 1) run_net<1>(a, xin, bA, bB, z, row0, nrows, red);
     else run_net<2>(a, xin, bA, bB, z, row0, nrows, red);
+  } else if (split) {
+    // the trunk output buffer and the (consumed) input tile are the head's ping-pong pair
+    float* t = run_net<0>(a, xin, bA, bB, z, row0, nrows, red, tsave);
+    if (lb.y == 0) run_net<1>(a, t, t, xin, z, row0, nrows, red);
+    else run_net<2>(a, t, t, xin, z, row0, nrows, red);
   } else {
     float* t = run_net<0>(a, xin, bA, bB, z, row0, nrows, red);
     // move the trunk output out of the ping-pong pair
@@ -338,7 +360,8 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
   int nbatch = 1;
   for (int j = 0; j < njobs; ++j) {
     const drpo_mlp_fwd_t* a = jobs_host + j;
-    DRPO_REQUIRE(a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1, "drpo_mlp_forward_multi: bad job %d", j);
+    DRPO_REQUIRE(a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1 && !a->split_heads,
+                 "drpo_mlp_forward_multi: bad job %d", j);
     const int din0 = a->cols[0] + a->cols[1] + a->cols[2];
     DRPO_REQUIRE(din0 >= 1 && din0 <= 256, "drpo_mlp_forward_multi: job %d input width %d", j, din0);
     if (a->trunk) {
@@ -396,7 +419,9 @@ DRPO_API int drpo_mlp_forward(const drpo_mlp_fwd_t* a, drpo_stream_t stream_) {
     for (int h = 0; h < a->nnets; ++h) DRPO_REQUIRE(check_net(a->net[h], din0), "drpo_mlp_forward: bad net %d", h);
   }
   if (a->rows == 0) return DRPO_OK;
-  dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS), a->trunk ? 1 : a->nnets, a->nbatch);
+  DRPO_REQUIRE(!a->split_heads || (a->trunk && a->nnets >= 2), "drpo_mlp_forward: split_heads needs a trunk + heads");
+  dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS),
+            a->trunk ? (a->split_heads ? a->nnets - 1 : 1) : a->nnets, a->nbatch);
   mlp_fwd_kernel<<<grid, FW_NT, fwd_lds(), stream>>>(*a);
   DRPO_LAUNCH_CHECK("mlp_forward");
   return DRPO_OK;
@@ -445,7 +470,7 @@ __device__ __forceinline__ float act_grad_saved(int act, float saved) {
 
 // G (LDS, width of the net output) -> gradient w.r.t. the net input (returned LDS buffer)
 __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__ net, float* G, float* bA, float* bB, int z, int64_t rows,
-                          int row0, int nrows, bool need_dx0) {
+                          int row0, int nrows, bool need_dx0, bool alt = false) {
   const int tid = threadIdx.x;
   float* cur = G;
   float sv[BW_PER];
@@ -454,7 +479,7 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__
     const drpo_mlp_bwd_layer_t& L = net.L[l];
     // descriptor fields into registers once per layer (no reloads inside the loops)
     const int dout = L.dout, din = L.din, act = L.act;
-    float* __restrict__ dzp = L.dz;
+    float* __restrict__ dzp = alt ? L.dz2 : L.dz;
     const float* W = L.W + (size_t)z * L.wstride;
     const size_t so = ((size_t)z * rows + row0) * dout;
     const int wpad = round_up(dout, 16);
@@ -485,14 +510,14 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__
 
 // one (job, net) slot of the fused backward-data pass; `a` may live in kernarg
 // (single launch) or global memory (multi-job launch)
-__device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, int sel, float* smem) {
+__device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, int sel, int bx, int bz, float* smem) {
   float* G = smem;
   float* bA = G + FW_ROWS * LDH;
   float* bB = bA + FW_ROWS * LDH;
   float* DT = bB + FW_ROWS * LDH;   // trunk output gradient accumulator
   const int tid = threadIdx.x;
-  const int z = blockIdx.z;
-  const int row0 = blockIdx.x * FW_ROWS;
+  const int z = bz;
+  const int row0 = bx * FW_ROWS;
   if (row0 >= a.rows) return;
   const int nrows = (int)min((int64_t)FW_ROWS, a.rows - row0);
 
@@ -522,6 +547,15 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     if (gx) store_dx(n, gx);
     return;
   }
+  if (a.split_heads) {
+    // head sel + 1 alone: the trunk gradient is linear in the head gradients, so its
+    // share backs through the trunk here (dz for head 1, dz2 for head 2)
+    const drpo_mlp_bwd_net_t& n = a.net[sel + 1];
+    load_gout(n, G);
+    float* gh = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, true);
+    bwd_net(a.net[0], gh, bA, bB, z, a.rows, row0, nrows, false, sel == 1);
+    return;
+  }
   const int tw = a.net[0].L[a.net[0].nl - 1].dout;
   const int twpad = round_up(tw, 16);
   for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) DT[(e / twpad) * LDH + e % twpad] = 0.f;
@@ -541,7 +575,8 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
 
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  bwd_body(a, blockIdx.y, smem);
+  const LogicalBlock lb = xcd_block();   // one member's tiles per XCD (shared weights in L2)
+  bwd_body(a, lb.y, lb.x, lb.z, smem);
 }
 
 struct BwdMultiArgs {
@@ -555,7 +590,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const drpo_mlp_bwd_t* __restrict__ ap = m.jobs + m.slot_job[blockIdx.y];
   const drpo_mlp_bwd_t& a = *ap;
   if (blockIdx.z >= (unsigned)a.nbatch) return;
-  bwd_body(a, m.slot_net[blockIdx.y], smem);
+  bwd_body(a, m.slot_net[blockIdx.y], blockIdx.x, blockIdx.z, smem);
 }
 
 static size_t bwd_lds() { return sizeof(float) * (size_t)4 * FW_ROWS * LDH; }
@@ -572,15 +607,23 @@ DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, drpo_stream_t stream_) {
                    "drpo_mlp_backward: bad layer %d of net %d", l, h);
     if (n.dx) DRPO_REQUIRE(n.dx_col0 >= 0 && n.dx_col0 + n.dx_cols <= n.L[0].din, "drpo_mlp_backward: dx columns");
   }
+  if (a->split_heads) {
+    DRPO_REQUIRE(a->trunk && a->nnets >= 2 && a->nnets <= 3 && !a->net[0].dx,
+                 "drpo_mlp_backward: split_heads needs a trunk, 1-2 heads and no trunk input gradient");
+    for (int l = 0; l < a->net[0].nl; ++l)
+      DRPO_REQUIRE(a->nnets < 3 || !a->net[0].L[l].dz == !a->net[0].L[l].dz2,
+                   "drpo_mlp_backward: split_heads trunk layer %d needs dz2 with dz", l);
+  }
   if (a->rows == 0) return DRPO_OK;
-  dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS), a->trunk ? 1 : a->nnets, a->nbatch);
+  dim3 grid((unsigned)((a->rows + FW_ROWS - 1) / FW_ROWS),
+            a->trunk ? (a->split_heads ? a->nnets - 1 : 1) : a->nnets, a->nbatch);
   mlp_bwd_kernel<<<grid, FW_NT, bwd_lds(), stream>>>(*a);
   DRPO_LAUNCH_CHECK("mlp_backward");
   return DRPO_OK;
 }
 
 static int check_bwd(const drpo_mlp_bwd_t* a) {
-  if (!(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1)) return 0;
+  if (!(a && a->nnets >= 1 && a->nnets <= MAXN && a->nbatch >= 1 && !a->split_heads)) return 0;
   for (int h = 0; h < a->nnets; ++h) {
     const drpo_mlp_bwd_net_t& n = a->net[h];
     if (!(n.nl >= 1 && n.nl <= MAXL && (n.gout || (a->trunk && h == 0)))) return 0;
@@ -665,11 +708,17 @@ __device__ __forceinline__ f32x4 wg_load4(const float* __restrict__ M, int64_t r
   return v;
 }
 
-__global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
+// PRE > 0: a chunk of at most PRE stages (the ensemble fit: 256 rows per member) is
+// loaded into registers all at once at the start, so the workgroup waits one memory
+// latency instead of one per stage (the streaming loop below keeps one stage in
+// flight); ~210 VGPRs, still 2 workgroups per CU.
+template <int PRE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRE ? 2 : 1))) void mlp_wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   float* Az = wsm;                                // [2][STAGE][LD]  dZ stage
   float* By = wsm + 2 * WG_STAGE * WG_LD;         // [2][STAGE][LD]  Y stage
-  const int64_t bid = blockIdx.x;
+  STAMPW(0);
+  const int64_t bid = xcd_block().x;   // tiles sharing a dZ / Y column block run on one XCD
   int q = 0;
   while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
   const drpo_wgrad_item_t& I = a.it[q];
@@ -715,13 +764,7 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;          // bias partial: column (tid & 63), rows (tid >> 6) + 4k of each stage
-  gload(r0);
-  sstore(0);
-  __syncthreads();
-  int buf = 0;
-  for (int64_t rb = r0; rb < r1; rb += WG_STAGE) {
-    const bool more = rb + WG_STAGE < r1;
-    if (more) gload(rb + WG_STAGE);
+  auto compute = [&](int buf) {
     const float* A = Az + buf * WG_STAGE * WG_LD;
     const float* Bm = By + buf * WG_STAGE * WG_LD;
 #pragma unroll
@@ -738,41 +781,80 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
 #pragma unroll
       for (int k = 0; k < WG_STAGE / 4; ++k) bsum += A[((tid >> 6) + 4 * k) * WG_LD + (tid & 63)];
     }
-    if (more) {
-      sstore(buf ^ 1);
+  };
+  if constexpr (PRE > 0) {
+    f32x4 qz[PRE][4], qy[PRE][4];
+#pragma unroll
+    for (int st = 0; st < PRE; ++st)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        qz[st][j] = wg_load4(dz, r0 + st * WG_STAGE + sr + 16 * j, r1, o0 + sc, I.dout, vz);
+        qy[st][j] = wg_load4(y, r0 + st * WG_STAGE + sr + 16 * j, r1, i0 + sc, I.din, vy);
+      }
+#pragma unroll
+    for (int st = 0; st < PRE; ++st) {
+      if (r0 + st * WG_STAGE >= r1) break;
+      // buffer st&1 was last read in stage st-2; every wave passed stage st-1's barrier
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        *reinterpret_cast<f32x4*>(&Az[((st & 1) * WG_STAGE + sr + 16 * j) * WG_LD + sc]) = qz[st][j];
+        *reinterpret_cast<f32x4*>(&By[((st & 1) * WG_STAGE + sr + 16 * j) * WG_LD + sc]) = qy[st][j];
+      }
       __syncthreads();
-      buf ^= 1;
+      if (st == 0) STAMPW(1);
+      compute(st & 1);
+    }
+  } else {
+    gload(r0);
+    sstore(0);
+    __syncthreads();
+    STAMPW(1);
+    int buf = 0;
+    for (int64_t rb = r0; rb < r1; rb += WG_STAGE) {
+      const bool more = rb + WG_STAGE < r1;
+      if (more) gload(rb + WG_STAGE);
+      compute(buf);
+      if (more) {
+        sstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
     }
   }
   __syncthreads();
-  // reduce the 4 waves' partial tiles: red[o_local][i_local] (64 x 64), waves add in turn
-  float* red = wsm;                               // 64 * 65 floats (reuses the stages)
-  constexpr int RL = 65;
+  STAMPW(2);
+  // Reduce the 4 waves' partial 64x64 tiles. Each wave stores its accumulators to its
+  // own LDS slab as R[w][m*4+n][rr][lane] (blocks of 272 floats: 256 + 16 pad), one
+  // conflict-free ds_write_b32 per register; after one barrier every thread sums the 4
+  // slabs for the 16 outputs it adds to global memory (rows ol = tid/64 + 4j, column
+  // il = tid%64: consecutive lanes read banks 16n + g*16 + l15, all distinct).
+  // (Was: the waves added into one padded tile in turn -- 4 barriers and 4-way
+  // conflicts, 7.7 k cycles per workgroup, as long as the MFMA work itself.)
+  float* R = wsm;
+  constexpr int RB = 272;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    if (wave == w) {
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int ol = 4 * (4 * g + rr) + m, il = 4 * l15 + n;
-            float* p = &red[ol * RL + il];
-            *p = (w == 0 ? 0.f : *p) + acc[m][n][rr];
-          }
-    }
-    __syncthreads();
-  }
+      for (int rr = 0; rr < 4; ++rr) R[(wave * 16 + m * 4 + n) * RB + rr * 64 + lane] = acc[m][n][rr];
+  __syncthreads();
+  STAMPW(3);
   float* gW = I.gW + (size_t)zb * I.gwstride;
-  for (int e = tid; e < WG_T * WG_T; e += 256) {
-    const int ol = e >> 6, il = e & 63;
-    const int o = o0 + ol, i = i0 + il;
-    if (o < I.dout && i < I.din) atomicAdd(&gW[(size_t)o * I.din + i], red[ol * RL + il]);
+  {
+    const int il = tid & 63, n = il & 3, l15 = il >> 2;
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      const int ol = (tid >> 6) + 4 * j;
+      const int m = ol & 3, gg = ol >> 4, rr = (ol >> 2) & 3;
+      const int off = (m * 4 + n) * RB + rr * 64 + gg * 16 + l15;
+      const float v = R[off] + R[16 * RB + off] + R[32 * RB + off] + R[48 * RB + off];
+      const int o = o0 + ol, i = i0 + il;
+      if (o < I.dout && i < I.din) atomicAdd(&gW[(size_t)o * I.din + i], v);
+    }
   }
   if (do_bias) {
-    __syncthreads();
-    float* bred = wsm + WG_T * RL;
+    float* bred = wsm + 64 * RB;
     bred[tid] = bsum;
     __syncthreads();
     if (tid < 64) {
@@ -781,9 +863,11 @@ __global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
       if (o < I.dout) atomicAdd(&I.gb[(size_t)zb * I.gbstride + o], v);
     }
   }
+  STAMPW(4);
 }
 
-static size_t wgrad_lds() { return sizeof(float) * (size_t)4 * WG_STAGE * WG_LD; }
+// max(two stages of dZ + Y, the 4 reduction slabs + bias partials)
+static size_t wgrad_lds() { return sizeof(float) * max((size_t)4 * WG_STAGE * WG_LD, (size_t)64 * 272 + 256); }
 
 DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
@@ -819,7 +903,13 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t
   a.first[m] = tot;
   a.n = m;
   if (tot == 0) return DRPO_OK;
-  mlp_wgrad_kernel<<<(unsigned)tot, 256, wgrad_lds(), stream>>>(a);
+  int64_t maxrows = 0;
+  for (int k = 0; k < m; ++k) maxrows = max(maxrows, a.it[k].rows);
+  static const bool pre_ok = getenv("DRPO_WGRAD_PRELOAD") && getenv("DRPO_WGRAD_PRELOAD")[0] == '1';
+  if (pre_ok && min((int64_t)a.chunk, maxrows) <= 4 * WG_STAGE)
+    mlp_wgrad_kernel<4><<<(unsigned)tot, 256, wgrad_lds(), stream>>>(a);
+  else
+    mlp_wgrad_kernel<0><<<(unsigned)tot, 256, wgrad_lds(), stream>>>(a);
   DRPO_LAUNCH_CHECK("mlp_wgrad");
   return DRPO_OK;
 }

@@ -255,6 +255,23 @@ __device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i
   float* P = mp->P;
   float* Pt = has_t ? mp->Pt : nullptr;
   float* PT = mp->PT;
+  if (n == 4 && (din & 3) == 0) {
+    // k is a multiple of 4 and k..k+3 stay in row o: the 4 forward-mirror components
+    // of one fragment lane are contiguous (one 16-byte store)
+    const int64_t base = mp->poff[l] + (int64_t)z * ncb * nks * 256;
+    const int64_t pi = base + ((int64_t)((o >> 4) * nks + (k >> 4)) << 8) + ((((k >> 2) & 3) * 16 + (o & 15)) << 2);
+    if (P) *reinterpret_cast<f32x4*>(P + pi) = f32x4{pv[0], pv[1], pv[2], pv[3]};
+    if (Pt) *reinterpret_cast<f32x4*>(Pt + pi) = f32x4{tv[0], tv[1], tv[2], tv[3]};
+    if (PT) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = k + e;
+        const int64_t ti = base + ((int64_t)((kk >> 4) * ncb + (o >> 4)) << 8) + ((((o >> 2) & 3) * 16 + (kk & 15)) << 2) + (o & 3);
+        PT[ti] = pv[e];
+      }
+    }
+    return;
+  }
   for (int e = 0; e < n; ++e) {
     const int64_t base = mp->poff[l] + (int64_t)z * ncb * nks * 256;
     // forward mirror: fragment (o>>4, k>>4), lane ((k>>2)&3)*16 + (o&15), component k&3
@@ -277,10 +294,19 @@ __device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i
 
 __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   __shared__ float s_coef;
+  // the segment's pack map, staged once per workgroup: the per-thread layer search
+  // of pack_write4 then reads LDS instead of a chain of dependent global loads
+  __shared__ __attribute__((aligned(16))) int s_map[(sizeof(drpo_pack_map_t) + 3) / 4];
   const int64_t bid = blockIdx.x;
   int q = 0;
   while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
   const drpo_optim_seg_t& S = a.seg[q];
+  if (S.map) {
+    const int* src = reinterpret_cast<const int*>(S.map);
+    for (int i = threadIdx.x; i < (int)(sizeof(drpo_pack_map_t) / 4); i += 256) s_map[i] = src[i];
+    __syncthreads();
+  }
+  const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
   if (S.partial) {
     if (threadIdx.x < 64) {
       float s = 0.f;
@@ -352,11 +378,11 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   }
   if (S.map) {
     if (vec) {
-      pack_write4(S.map, i0, 4, p, t, S.ema_target != nullptr);
+      pack_write4(map, i0, 4, p, t, S.ema_target != nullptr);
     } else {
       for (int e = 0; e < n; ++e) {
         const float pe[4] = {p[e], 0.f, 0.f, 0.f}, te[4] = {t[e], 0.f, 0.f, 0.f};
-        pack_write4(S.map, i0 + e, 1, pe, te, S.ema_target != nullptr);
+        pack_write4(map, i0 + e, 1, pe, te, S.ema_target != nullptr);
       }
     }
   }

@@ -18,6 +18,7 @@ The per-step ``loss.item()`` of the reference is deferred: losses land in a devi
 array that is read once at the end of fit (same returned list of floats).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -27,6 +28,26 @@ from .optim import fused_step
 from .rng import DeviceNoise
 from .sac_step import ACT_ID, Net, fill_bwd, fill_fwd
 from ._abi import WgradItem
+
+
+# Forward: one workgroup per (row tile, head) when the plain grid (16-row tiles x
+# members) would leave most of the 256 CUs idle. The trunk is recomputed per head
+# (1.33x the forward FLOPs) but each workgroup's serial chain shortens from 5 to 3
+# dense layers: fit forward 28.8 -> 20.1 us at E=7, b=256 (csrc/mlp.hip, split_heads).
+# Backward: the same split (2 instead of 4 dense layers per workgroup, 33.8 -> 22.7 us)
+# leaves the trunk dZ as two terms, and the weight-gradient pass then re-reads the
+# trunk activations once per term (21 -> 38 us), so it is off unless DRPO_SPLIT_BWD=1.
+SPLIT_HEADS_MAX_TILES = 256
+
+
+def split_heads(n, Z):
+    if os.environ.get('DRPO_SPLIT_HEADS', '1') == '0':
+        return False
+    return (n + 15) // 16 * Z <= SPLIT_HEADS_MAX_TILES
+
+
+def split_heads_bwd(n, Z):
+    return os.environ.get('DRPO_SPLIT_BWD', '0') == '1' and split_heads(n, Z)
 
 
 class EnsembleEngine:
@@ -93,12 +114,15 @@ class EnsembleEngine:
         m.group.ensure_packed()
         nets, strides = self._nets(member, grads=save, z0=z0)
         rows = Z * n
+        split = split_heads(n, Z)
         if save:
             for j, net in enumerate(nets):
                 for l, (_, _, din, dout, act, _) in enumerate(net.layers):
                     net.sy[l] = self.buf(f'{tag}.sy{j}{l}', rows, dout)
                     net.sz[l] = self.buf(f'{tag}.sz{j}{l}', rows, dout) if act == ACT_ID['swish'] else None
                     net.dz[l] = self.buf(f'{tag}.dz{j}{l}', rows, dout)
+                    if j == 0 and split_heads_bwd(n, Z):
+                        net.dz2[l] = self.buf(f'{tag}.dzb{l}', rows, dout)
             save_x = self.buf(f'{tag}.x', rows, S + A)
         else:
             save_x = None
@@ -106,7 +130,7 @@ class EnsembleEngine:
             nets[2].sy[-1] = self.buf(f'{tag}.L', rows, S1)
         norm = m.state_normalizer
         d = fill_fwd(nets, [(s, S), (a, A)], n, trunk=True, save_x=save_x, norm=(norm.mean, norm.std), nbatch=Z,
-                     wstride=strides, sstride=[s_zs, a_zs, 0])
+                     wstride=strides, sstride=[s_zs, a_zs, 0], split_heads=split)
         return d, nets, strides, save_x
 
     def _forward(self, s, a, n, Z, s_zs, a_zs, member=None, tag='f', save=False, z0=0):
@@ -220,18 +244,24 @@ class EnsembleEngine:
         return mse, gD, gL
 
     def _backward_descs(self, nets, strides, save_x, gD, gL, b, Z):
-        d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides)
+        split = nets[0].dz2[0] is not None
+        d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides, split_heads=split)
         items = []
         trunk_out = nets[0].sy[-1]
         for j, net in enumerate(nets):
             ins = [save_x if j == 0 else trunk_out] + [net.sy[l] for l in range(len(net.layers) - 1)]
             for l, (W, bb, din, dout, act, _) in enumerate(net.layers):
                 gW, gb = net.grad_layers[l]
-                it = WgradItem()
-                it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
-                it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
-                it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
-                items.append(it)
+                # split heads: the trunk dZ is dz + dz2, one item per term (both add into
+                # the zeroed gradient: two float adds onto 0 commute, so still deterministic)
+                for dz in (net.dz[l], net.dz2[l]):
+                    if dz is None:
+                        continue
+                    it = WgradItem()
+                    it.dz, it.y, it.gW, it.gb = dz.data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
+                    it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
+                    it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
+                    items.append(it)
         return d, (WgradItem * len(items))(*items), len(items)
 
     def _backward(self, nets, strides, save_x, gD, gL, b, Z):

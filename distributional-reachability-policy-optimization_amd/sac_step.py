@@ -52,6 +52,7 @@ class Net:
         self.sy = [None] * len(layers)
         self.sz = [None] * len(layers)
         self.dz = [None] * len(layers)
+        self.dz2 = [None] * len(layers)   # split-heads trunk: the second head's dZ share
 
     @property
     def dout(self):
@@ -71,7 +72,8 @@ def noise_tag(eps):
     return '.p' if eps is not None else '.d'
 
 
-def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, wstride=None, sstride=None):
+def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, wstride=None, sstride=None,
+             split_heads=False):
     d = MlpFwd()
     for k, (t, cols) in enumerate(srcs):
         d.src[k] = _p(t)
@@ -88,11 +90,13 @@ def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, ws
             L.sy, L.sz = _p(net.sy[l]), _p(net.sz[l])
             L.wstride, L.bstride = (0, 0) if wstride is None else wstride[j][l]
     d.nnets, d.trunk, d.rows, d.nbatch = len(nets), int(trunk), rows, nbatch
+    d.split_heads = int(split_heads)
     return d
 
 
-def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None):
-    """nets[0] trunk when trunk=True (gouts[0] ignored); dx: {net_index: (tensor, col0, cols, accumulate)}."""
+def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None, split_heads=False):
+    """nets[0] trunk when trunk=True (gouts[0] ignored); dx: {net_index: (tensor, col0, cols, accumulate)};
+    split_heads: one workgroup per head, the second head's trunk dZ share into nets[0].dz2."""
     d = MlpBwd()
     for j, net in enumerate(nets):
         d.net[j].nl = len(net.layers)
@@ -101,12 +105,14 @@ def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None):
             assert WT is not None, 'backward needs the transposed weight mirror (trained group)'
             L.W, L.din, L.dout, L.act = WT.data_ptr(), din, dout, act
             L.sy, L.sz, L.dz = _p(net.sy[l]), _p(net.sz[l]), _p(net.dz[l])
+            L.dz2 = _p(net.dz2[l]) if getattr(net, 'dz2', None) else 0
             L.wstride = 0 if wstride is None else wstride[j][l][0]
         d.net[j].gout = _p(gouts[j])
         if dx and j in dx:
             t, c0, nc, accum = dx[j]
             d.net[j].dx, d.net[j].dx_col0, d.net[j].dx_cols, d.net[j].dx_accumulate = t.data_ptr(), c0, nc, int(accum)
     d.nnets, d.trunk, d.rows, d.nbatch = len(nets), int(trunk), rows, nbatch
+    d.split_heads = int(split_heads)
     return d
 
 

@@ -156,6 +156,9 @@ typedef struct {
   int64_t rows;
   int nbatch;
   drpo_policy_head_t head;   /* multi-job launches only (mode 0 elsewhere) */
+  int split_heads;     /* trunk mode, single launches: one workgroup per (row tile, head); each
+                          recomputes the trunk (only head 1's workgroup saves it) -- twice the
+                          workgroups for small ensembles (fit: 16 tiles x 7 members) */
 } drpo_mlp_fwd_t;
 
 typedef struct {
@@ -165,6 +168,8 @@ typedef struct {
   const float* sz;
   float* dz;           /* optional save of dL/dZ for weight gradients */
   int64_t wstride;
+  float* dz2;          /* split_heads trunk layers: the second head's partial dL/dZ (trunk
+                          dZ = dz + dz2: one wgrad item per term, both accumulate into dW) */
 } drpo_mlp_bwd_layer_t;
 
 typedef struct {
@@ -181,6 +186,9 @@ typedef struct {
   int trunk;
   int64_t rows;
   int nbatch;
+  int split_heads;     /* trunk mode, single launches, trunk dx unused: one workgroup per (row
+                          tile, head) backs its head's gradient through the trunk (linear in
+                          the head gradients), writing dz (head 1) / dz2 (head 2) */
 } drpo_mlp_bwd_t;
 
 typedef struct {
