@@ -57,7 +57,8 @@ DRPO_API int drpo_debug_stamps(unsigned long long* dst, int n) {
     unsigned long long _t;                                                                        \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
     __builtin_amdgcn_sched_barrier(0);                                                            \
-    if (threadIdx.x == 0 && blockIdx.x < 32768u) g_stamps[32768 + blockIdx.x][(i)] = _t;          \
+    const unsigned _w = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);          \
+    if (threadIdx.x == 0 && _w < 32768u) g_stamps[32768 + _w][(i)] = _t;                          \
   } while (0)
 #else
 #define STAMP(i) \
@@ -558,19 +559,25 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
   }
   const int tw = a.net[0].L[a.net[0].nl - 1].dout;
   const int twpad = round_up(tw, 16);
+  STAMPW(5);
   for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) DT[(e / twpad) * LDH + e % twpad] = 0.f;
   lds_barrier();
   for (int h = 1; h < a.nnets; ++h) {
     load_gout(a.net[h], G);
+    if (h == 1) STAMPW(6); else STAMPW(9);
     const float* gh = bwd_net(a.net[h], G, bA, bB, z, a.rows, row0, nrows, true);
+    if (h == 1) STAMPW(7); else STAMPW(10);
     for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) {
       const int r = e / twpad, k = e - r * twpad;
       DT[r * LDH + k] += gh[r * LDH + k];
     }
     lds_barrier();
+    if (h == 1) STAMPW(8); else STAMPW(11);
   }
   const float* gx = bwd_net(a.net[0], DT, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
+  STAMPW(12);
   if (gx) store_dx(a.net[0], gx);
+  STAMPW(13);
 }
 
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {

@@ -43,6 +43,17 @@ def main():
         print(f'   {names[c - 1]:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
     d = st[:, 4] - st[:, 0]
     print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
+    bw = buf[32768:32768 + 4096, 5:14].astype(np.int64)
+    nb = int((bw[:, 8] > 0).sum())
+    bw = bw[:nb]
+    print(f'== mlp_bwd_kernel (fit step, trunk + 2 heads): {nb} workgroups')
+    names = ['head 1 gout load', 'head 1 backward', 'head 1 add to dT', 'head 2 gout load', 'head 2 backward',
+             'head 2 add to dT', 'trunk backward', 'dx store']
+    for c in range(1, 9):
+        d = bw[:, c] - bw[:, c - 1]
+        print(f'   {names[c - 1]:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
+    d = bw[:, 8] - bw[:, 0]
+    print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
 
 
 if __name__ == '__main__':
