@@ -50,6 +50,12 @@ class OptimSeg(ctypes.Structure):
                 ('ema_target', P), ('ema_rate', c_float), ('ema_keep', c_float), ('map', P)]
 
 
+class EnsReduce(ctypes.Structure):
+    """drpo_ens_reduce_t"""
+    _fields_ = [('part', P), ('nbx', c_int), ('Z', c_int), ('S1', c_int), ('minlv', P), ('maxlv', P),
+                ('weight', c_float), ('gscale', P), ('mse', P), ('loss', P), ('gmin', P), ('gmax', P)]
+
+
 # name -> (restype, argtypes)
 PROTOTYPES = {
     'drpo_version': (c_int, []),
@@ -85,6 +91,8 @@ PROTOTYPES = {
     'drpo_ens_loss_workspace_size': (c_size_t, [c_int64, c_int, c_int]),
     'drpo_ens_loss': (c_int, [P, P, P, c_int64, P, c_int64, c_int64, c_int, c_int, P, P, c_float, P, P, P, P, P, P,
                               P, P, P]),
+    'drpo_ens_loss_partials': (c_int, [P, P, P, c_int64, P, c_int64, c_int64, c_int, c_int, P, P, c_float, P, P, P,
+                                       P, P, P, P, P, POINTER(EnsReduce), P]),
 }
 
 
@@ -164,6 +172,7 @@ PROTOTYPES.update({
     'drpo_mlp_backward_multi': (c_int, [POINTER(MlpBwd), P, c_int, P]),
     'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
     'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P]),
+    'drpo_mlp_wgrad_reduce': (c_int, [POINTER(WgradItem), c_int, POINTER(EnsReduce), P]),
     'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
                                   c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
     'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,

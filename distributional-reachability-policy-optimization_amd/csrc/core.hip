@@ -59,6 +59,7 @@ DRPO_API int64_t drpo_abi_sizeof(const char* name) {
       {"drpo_wgrad_item_t", sizeof(drpo_wgrad_item_t)},     {"drpo_buffer_view_t", sizeof(drpo_buffer_view_t)},
       {"drpo_critic_head_t", sizeof(drpo_critic_head_t)},   {"drpo_pack_item_t", sizeof(drpo_pack_item_t)},
       {"drpo_pack_map_t", sizeof(drpo_pack_map_t)},         {"drpo_optim_seg_t", sizeof(drpo_optim_seg_t)},
+      {"drpo_ens_reduce_t", sizeof(drpo_ens_reduce_t)},
   };
   for (const E& e : table)
     if (strcmp(e.n, name) == 0) return (int64_t)e.s;

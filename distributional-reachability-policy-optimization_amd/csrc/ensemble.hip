@@ -13,6 +13,7 @@
 //                   (src/dynamics.py:143-153,236-253)
 // All are HBM/latency-bound epilogues; the GEMM work is in mlp.hip.
 #include "common.hpp"
+#include "ens_reduce.hpp"
 
 using namespace drpo;
 
@@ -160,7 +161,6 @@ DRPO_API int drpo_ens_head(const float* D, const float* LVR, const float* s, int
 // bound gradients: deterministic, no memset, and no in-kernel cross-workgroup hand-
 // off (a device-scope fence writes back the whole XCD L2 on gfx950: measured 22 us
 // for a last-block variant of this kernel).
-constexpr int LOSS_MAXS1 = 256;
 
 __global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__ D, const float* __restrict__ LVR,
                                                        const float* __restrict__ s, int64_t s_zstride,
@@ -224,67 +224,9 @@ __global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__
   }
 }
 
-// per-member NLL, total loss, bound gradients from the block partials. Every sum is
-// spread over 16 lanes (strided partials, then a fixed xor tree), so the kernel waits
-// a couple of memory latencies instead of one per partial; the order is fixed, so the
-// result is deterministic.
-__global__ __launch_bounds__(256) void ens_loss_reduce_kernel(const float* __restrict__ part, int nbx, int Z, int S1,
-                                                              const float* __restrict__ minlv,
-                                                              const float* __restrict__ maxlv, float weight,
-                                                              const float* gscale, float* mse, float* loss,
-                                                              float* gmin, float* gmax) {
-  __shared__ float red[256], smx[LOSS_MAXS1], smn[LOSS_MAXS1];
-  const int tid = threadIdx.x;
-  const int grp = tid >> 4, l16 = tid & 15;
-  const float* part_mse = part;
-  const float* part_min = part_mse + (size_t)Z * nbx;
-  const float* part_max = part_min + (size_t)Z * nbx * S1;
-  for (int z = grp; z < Z; z += 16) {
-    float m = 0.f;
-    for (int q = l16; q < nbx; q += 16) m += part_mse[(size_t)z * nbx + q];
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) m += __shfl_xor(m, o, 16);
-    if (l16 == 0) {
-      mse[z] = m;
-      red[z] = m;
-    }
-  }
-  const size_t Q = (size_t)Z * nbx;
-  const float gw = gmin ? (gscale ? *gscale : 1.f) * weight : 0.f;
-  for (int c = grp; c < S1; c += 16) {
-    if (gmin) {
-      float a0 = 0.f, a1 = 0.f;
-      for (size_t q = l16; q < Q; q += 16) {
-        a0 += part_min[q * S1 + c];
-        a1 += part_max[q * S1 + c];
-      }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) {
-        a0 += __shfl_xor(a0, o, 16);
-        a1 += __shfl_xor(a1, o, 16);
-      }
-      if (l16 == 0) {
-        gmin[c] += a0 - gw;
-        gmax[c] += a1 + gw;
-      }
-    }
-    if (l16 == 0) {
-      smx[c] = maxlv[c];
-      smn[c] = minlv[c];
-    }
-  }
-  __syncthreads();
-  if (tid == 0 && loss) {
-    float tot = 0.f;
-    for (int zz = 0; zz < Z; ++zz) tot += red[zz];
-    float smax = 0.f, smin = 0.f;
-    for (int kk = 0; kk < S1; ++kk) {
-      smax += smx[kk];
-      smin += smn[kk];
-    }
-    *loss = tot + weight * (smax - smin);
-  }
-}
+// per-member NLL, total loss, bound gradients from the block partials
+// (ens_reduce.hpp; also run as the last block of a drpo_mlp_wgrad_reduce launch)
+__global__ __launch_bounds__(256) void ens_loss_reduce_kernel(drpo_ens_reduce_t r) { ens_loss_reduce_block(r); }
 
 // rows per loss workgroup: one row per thread (256 / KP rows of KP column lanes)
 static int loss_rows(int S1);
@@ -303,10 +245,11 @@ DRPO_API size_t drpo_ens_loss_workspace_size(int64_t b, int S, int Z) {
   return sizeof(float) * (size_t)Z * nbx * (1 + 2 * (size_t)(S + 1));
 }
 
-DRPO_API int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
+static int ens_loss_launch(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
                            int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv,
                            float weight, const float* gscale, float* mse, float* loss, float* gD, float* gLVR,
-                           float* gmin, float* gmax, void* workspace, drpo_stream_t stream_) {
+                           float* gmin, float* gmax, void* workspace, drpo_ens_reduce_t* reduce_out,
+                           drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(D && LVR && s && t && minlv && maxlv && mse && workspace && b >= 1 && S >= 1 &&
                    S + 1 <= LOSS_MAXS1 && Z >= 1,
@@ -321,8 +264,30 @@ DRPO_API int drpo_ens_loss(const float* D, const float* LVR, const float* s, int
                                                              loss_kp(S + 1), minlv, maxlv, gscale, gD, gLVR,
                                                              (float*)workspace);
   DRPO_LAUNCH_CHECK("ens_loss");
-  ens_loss_reduce_kernel<<<1, 256, 0, stream>>>((const float*)workspace, nbx, Z, S + 1, minlv, maxlv, weight, gscale,
-                                                mse, loss, gmin, gmax);
+  const drpo_ens_reduce_t r{(const float*)workspace, nbx, Z, S + 1, minlv, maxlv, weight, gscale, mse, loss, gmin, gmax};
+  if (reduce_out) {
+    *reduce_out = r;   // deferred: the caller runs it (drpo_mlp_wgrad_reduce)
+    return DRPO_OK;
+  }
+  ens_loss_reduce_kernel<<<1, 256, 0, stream>>>(r);
   DRPO_LAUNCH_CHECK("ens_loss_reduce");
   return DRPO_OK;
+}
+
+DRPO_API int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
+                           int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv,
+                           float weight, const float* gscale, float* mse, float* loss, float* gD, float* gLVR,
+                           float* gmin, float* gmax, void* workspace, drpo_stream_t stream) {
+  return ens_loss_launch(D, LVR, s, s_zstride, t, t_zstride, b, S, Z, minlv, maxlv, weight, gscale, mse, loss, gD,
+                         gLVR, gmin, gmax, workspace, nullptr, stream);
+}
+
+DRPO_API int drpo_ens_loss_partials(const float* D, const float* LVR, const float* s, int64_t s_zstride,
+                                    const float* t, int64_t t_zstride, int64_t b, int S, int Z, const float* minlv,
+                                    const float* maxlv, float weight, const float* gscale, float* mse, float* loss,
+                                    float* gD, float* gLVR, float* gmin, float* gmax, void* workspace,
+                                    drpo_ens_reduce_t* reduce_out, drpo_stream_t stream) {
+  DRPO_REQUIRE(reduce_out, "drpo_ens_loss_partials: reduce_out is required");
+  return ens_loss_launch(D, LVR, s, s_zstride, t, t_zstride, b, S, Z, minlv, maxlv, weight, gscale, mse, loss, gD,
+                         gLVR, gmin, gmax, workspace, reduce_out, stream);
 }

@@ -16,6 +16,7 @@
 #include <stdlib.h>
 
 #include "common.hpp"
+#include "ens_reduce.hpp"
 
 using namespace drpo;
 
@@ -700,6 +701,8 @@ struct WgradArgs {
   int64_t first[WG_MAXITEMS + 1];
   int n;
   int chunk;                        // rows per workgroup (multiple of WG_STAGE)
+  int has_red;                      // one extra (logically last) workgroup: loss reduction
+  drpo_ens_reduce_t red;
 };
 
 // rows [r, r+1) x 64 columns [c0, c0+64) of a row-major [rows][ld] matrix -> 16 floats
@@ -715,17 +718,16 @@ __device__ __forceinline__ f32x4 wg_load4(const float* __restrict__ M, int64_t r
   return v;
 }
 
-// PRE > 0: a chunk of at most PRE stages (the ensemble fit: 256 rows per member) is
-// loaded into registers all at once at the start, so the workgroup waits one memory
-// latency instead of one per stage (the streaming loop below keeps one stage in
-// flight); ~210 VGPRs, still 2 workgroups per CU.
-template <int PRE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRE ? 2 : 1))) void mlp_wgrad_kernel(WgradArgs a) {
+__global__ __launch_bounds__(256) void mlp_wgrad_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   float* Az = wsm;                                // [2][STAGE][LD]  dZ stage
   float* By = wsm + 2 * WG_STAGE * WG_LD;         // [2][STAGE][LD]  Y stage
   STAMPW(0);
   const int64_t bid = xcd_block().x;   // tiles sharing a dZ / Y column block run on one XCD
+  if (a.has_red && bid == a.first[a.n]) {
+    ens_loss_reduce_block(a.red);
+    return;
+  }
   int q = 0;
   while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
   const drpo_wgrad_item_t& I = a.it[q];
@@ -789,29 +791,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRE ? 2 : 1
       for (int k = 0; k < WG_STAGE / 4; ++k) bsum += A[((tid >> 6) + 4 * k) * WG_LD + (tid & 63)];
     }
   };
-  if constexpr (PRE > 0) {
-    f32x4 qz[PRE][4], qy[PRE][4];
-#pragma unroll
-    for (int st = 0; st < PRE; ++st)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        qz[st][j] = wg_load4(dz, r0 + st * WG_STAGE + sr + 16 * j, r1, o0 + sc, I.dout, vz);
-        qy[st][j] = wg_load4(y, r0 + st * WG_STAGE + sr + 16 * j, r1, i0 + sc, I.din, vy);
-      }
-#pragma unroll
-    for (int st = 0; st < PRE; ++st) {
-      if (r0 + st * WG_STAGE >= r1) break;
-      // buffer st&1 was last read in stage st-2; every wave passed stage st-1's barrier
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        *reinterpret_cast<f32x4*>(&Az[((st & 1) * WG_STAGE + sr + 16 * j) * WG_LD + sc]) = qz[st][j];
-        *reinterpret_cast<f32x4*>(&By[((st & 1) * WG_STAGE + sr + 16 * j) * WG_LD + sc]) = qy[st][j];
-      }
-      __syncthreads();
-      if (st == 0) STAMPW(1);
-      compute(st & 1);
-    }
-  } else {
+  {
     gload(r0);
     sstore(0);
     __syncthreads();
@@ -876,7 +856,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRE ? 2 : 1
 // max(two stages of dZ + Y, the 4 reduction slabs + bias partials)
 static size_t wgrad_lds() { return sizeof(float) * max((size_t)4 * WG_STAGE * WG_LD, (size_t)64 * 272 + 256); }
 
-DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t stream_) {
+DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t stream) {
+  return drpo_mlp_wgrad_reduce(items, n, nullptr, stream);
+}
+
+DRPO_API int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red,
+                                   drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS, "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
   WgradArgs a{};
@@ -909,14 +894,16 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, drpo_stream_t
   }
   a.first[m] = tot;
   a.n = m;
-  if (tot == 0) return DRPO_OK;
-  int64_t maxrows = 0;
-  for (int k = 0; k < m; ++k) maxrows = max(maxrows, a.it[k].rows);
-  static const bool pre_ok = getenv("DRPO_WGRAD_PRELOAD") && getenv("DRPO_WGRAD_PRELOAD")[0] == '1';
-  if (pre_ok && min((int64_t)a.chunk, maxrows) <= 4 * WG_STAGE)
-    mlp_wgrad_kernel<4><<<(unsigned)tot, 256, wgrad_lds(), stream>>>(a);
-  else
-    mlp_wgrad_kernel<0><<<(unsigned)tot, 256, wgrad_lds(), stream>>>(a);
+  if (red) {
+    DRPO_REQUIRE(red->part && red->mse && red->Z >= 1 && red->Z <= 256 && red->S1 >= 1 && red->S1 <= LOSS_MAXS1 &&
+                     red->nbx >= 1,
+                 "drpo_mlp_wgrad_reduce: bad reduction");
+    a.has_red = 1;
+    a.red = *red;
+  }
+  const int64_t blocks = tot + (red ? 1 : 0);
+  if (blocks == 0) return DRPO_OK;
+  mlp_wgrad_kernel<<<(unsigned)blocks, 256, wgrad_lds(), stream>>>(a);
   DRPO_LAUNCH_CHECK("mlp_wgrad");
   return DRPO_OK;
 }

@@ -27,7 +27,7 @@ from . import _lib
 from .optim import fused_step
 from .rng import DeviceNoise
 from .sac_step import ACT_ID, Net, fill_bwd, fill_fwd
-from ._abi import WgradItem
+from ._abi import EnsReduce, WgradItem
 
 
 # Forward: one workgroup per (row tile, head) when the plain grid (16-row tiles x
@@ -345,6 +345,7 @@ class EnsembleEngine:
         largs, _, gD, gL = self._loss_args(nets, xs, b * S, xt, b * S1, b, Z, True, loss_out=losses[0:1], tag='fit',
                                            bound=sh is None or sh.rank == 0)
         bd, warr, nw = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
+        red = EnsReduce()
         full = E * b if sh is not None else rows
         idx_all = None
         if nz.parity and steps > 0:
@@ -363,9 +364,10 @@ class EnsembleEngine:
             _lib.check(L.drpo_ens_gather(*gargs, idx, nz.seed, ctr, *gouts), 'ens_gather')
             _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
             largs[14] = ctypes.c_void_p(loss_base + 4 * i)
-            _lib.check(L.drpo_ens_loss(*largs, stream), 'ens_loss')
+            # the loss reduction rides as the last workgroup of the wgrad launch
+            _lib.check(L.drpo_ens_loss_partials(*largs, ctypes.byref(red), stream), 'ens_loss')
             _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
-            _lib.check(L.drpo_mlp_wgrad(warr, nw, stream), 'ensemble wgrad')
+            _lib.check(L.drpo_mlp_wgrad_reduce(warr, nw, ctypes.byref(red), stream), 'ensemble wgrad')
             if sh is None:
                 self.dp.mean_(g.grad)
             else:

@@ -202,6 +202,16 @@ typedef struct {
   int nbatch;
 } drpo_wgrad_item_t;
 
+/* the reduction step of drpo_ens_loss, as data: run by drpo_mlp_wgrad_reduce */
+typedef struct {
+  const float* part;   /* the loss workspace */
+  int nbx, Z, S1;
+  const float *minlv, *maxlv;
+  float weight;
+  const float* gscale;
+  float *mse, *loss, *gmin, *gmax;
+} drpo_ens_reduce_t;
+
 int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);
 /* Up to 8 independent forward jobs (different inputs / nets, e.g. every forward of
  * one SAC loss that does not depend on another) in ONE launch, each with an
@@ -214,6 +224,10 @@ int drpo_mlp_backward(const drpo_mlp_bwd_t* desc /* host */, drpo_stream_t strea
 int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
                             drpo_stream_t stream);
 int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, drpo_stream_t stream);
+/* drpo_mlp_wgrad plus one extra workgroup running a deferred ensemble-loss
+ * reduction (drpo_ens_loss_partials); red may be NULL */
+int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items /* host */, int n, const drpo_ens_reduce_t* red /* host */,
+                          drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- packed weight mirrors
  * Every MLP kernel streams weights from fragment-linear mirrors of the PyTorch
@@ -328,6 +342,15 @@ int drpo_ens_loss(const float* D, const float* LVR, const float* s, int64_t s_zs
                   int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv, float weight,
                   const float* gscale, float* mse, float* loss, float* gD, float* gLVR, float* gmin, float* gmax,
                   void* workspace, drpo_stream_t stream);
+/* drpo_ens_loss without its reduction launch: the reduction is described in
+ * *reduce_out and runs as the extra last workgroup of the next
+ * drpo_mlp_wgrad_reduce (the fit step's weight-gradient launch, which the
+ * reduction does not depend on) -- one launch fewer per fit step. */
+int drpo_ens_loss_partials(const float* D, const float* LVR, const float* s, int64_t s_zstride, const float* t,
+                           int64_t t_zstride, int64_t b, int S, int Z, const float* minlv, const float* maxlv,
+                           float weight, const float* gscale, float* mse, float* loss, float* gD, float* gLVR,
+                           float* gmin, float* gmax, void* workspace, drpo_ens_reduce_t* reduce_out,
+                           drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam (coupled L2), clip_grad_norm_, update_ema (src/ssac.py:446-455,

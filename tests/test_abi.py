@@ -78,7 +78,8 @@ def test_struct_layouts_match(built):
              'drpo_policy_head_t': A.PolicyHead, 'drpo_mlp_fwd_t': A.MlpFwd, 'drpo_mlp_bwd_layer_t': A.MlpBwdLayer,
              'drpo_mlp_bwd_net_t': A.MlpBwdNet, 'drpo_mlp_bwd_t': A.MlpBwd, 'drpo_wgrad_item_t': A.WgradItem,
              'drpo_buffer_view_t': A.BufferView, 'drpo_critic_head_t': A.CriticHead,
-             'drpo_pack_item_t': A.PackItem, 'drpo_pack_map_t': A.PackMap, 'drpo_optim_seg_t': A.OptimSeg}
+             'drpo_pack_item_t': A.PackItem, 'drpo_pack_map_t': A.PackMap, 'drpo_optim_seg_t': A.OptimSeg,
+             'drpo_ens_reduce_t': A.EnsReduce}
     for name, cls in pairs.items():
         assert built.drpo_abi_sizeof(name.encode()) == ctypes.sizeof(cls), name
     assert built.drpo_abi_sizeof(b'nope') == -1
