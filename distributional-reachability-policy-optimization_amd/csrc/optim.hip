@@ -301,36 +301,18 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   int q = 0;
   while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
   const drpo_optim_seg_t& S = a.seg[q];
-  if (S.map) {
-    const int* src = reinterpret_cast<const int*>(S.map);
-    for (int i = threadIdx.x; i < (int)(sizeof(drpo_pack_map_t) / 4); i += 256) s_map[i] = src[i];
-    __syncthreads();
-  }
-  const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
-  if (S.partial) {
-    if (threadIdx.x < 64) {
-      float s = 0.f;
-      for (int i = threadIdx.x; i < S.n_partial; i += 64) s += S.partial[i];
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-      if (threadIdx.x == 0) {
-        const float c = S.max_norm / (sqrtf(s) + 1e-6f);
-        s_coef = c < 1.f ? c : 1.f;
-      }
-    }
-    __syncthreads();
-  }
-  const float coef = S.partial ? s_coef : 1.f;
   const int64_t e0 = S.start + (bid - a.first[q]) * OPT_BLOCK_ELEMS;
   const int64_t e1 = min(S.end, e0 + OPT_BLOCK_ELEMS);
-  // Each thread owns 4 consecutive elements: all of its loads are issued before any
-  // arithmetic (one 16-byte load per array when the segment start is 4-aligned), so
-  // a block waits one memory latency instead of one per element.
+  // Each thread owns 4 consecutive elements. Its element loads are issued FIRST, so
+  // they are in flight together with the pack-map staging and the clip partial sums
+  // (one memory latency per workgroup instead of three in a row: the element loads
+  // depend on neither).
   const int64_t i0 = e0 + 4 * (int64_t)threadIdx.x;
-  if (i0 >= e1) return;
-  const int n = (int)min((int64_t)4, e1 - i0);
+  const bool live = i0 < e1;
+  const int n = live ? (int)min((int64_t)4, e1 - i0) : 0;
   const bool vec = n == 4 && (S.start & 3) == 0;
-  float p[4], g[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f}, v[4] = {0.f, 0.f, 0.f, 0.f};
-  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  float p[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f};
+  float v[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
   auto ld4 = [&](const float* src, float (&dst)[4]) {
     if (vec) {
       const f32x4 x = *reinterpret_cast<const f32x4*>(src + i0);
@@ -346,13 +328,37 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
       for (int e = 0; e < n; ++e) dst[i0 + e] = src[e];
     }
   };
-  ld4(S.p, p);
-  if (S.adam) {
-    ld4(S.g, g);
-    ld4(S.m, m);
-    ld4(S.v, v);
+  if (live) {
+    ld4(S.p, p);
+    if (S.adam) {
+      ld4(S.g, g);
+      ld4(S.m, m);
+      ld4(S.v, v);
+    }
+    if (S.ema_target) ld4(S.ema_target, t);
   }
-  if (S.ema_target) ld4(S.ema_target, t);
+  if (S.map) {
+    const int* src = reinterpret_cast<const int*>(S.map);
+    for (int i = threadIdx.x; i < (int)(sizeof(drpo_pack_map_t) / 4); i += 256) s_map[i] = src[i];
+  }
+  if (S.partial && threadIdx.x < 64) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < S.n_partial; i += 64) s += S.partial[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (threadIdx.x == 0) {
+      const float c = S.max_norm / (sqrtf(s) + 1e-6f);
+      s_coef = c < 1.f ? c : 1.f;
+    }
+  }
+  if (S.map || S.partial) __syncthreads();
+  const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
+  const float coef = S.partial ? s_coef : 1.f;
+  if (!live) return;
+  if (S.grad_from_sum) {   // SAC temperature: -exp(log_alpha) * alpha-loss sum / rows
+    const float gs = *S.grad_from_sum * (1.f / (float)S.grad_sum_rows);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[e] = -expf(p[e]) * gs;
+  }
   if (S.adam) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -396,6 +402,7 @@ DRPO_API int drpo_optim_step(const drpo_optim_seg_t* segs, int n, drpo_stream_t 
   for (int k = 0; k < n; ++k) {
     const drpo_optim_seg_t& S = segs[k];
     DRPO_REQUIRE(S.p && S.end >= S.start && (!S.adam || (S.g && S.m && S.v)), "drpo_optim_step: bad segment %d", k);
+    DRPO_REQUIRE(!S.grad_from_sum || S.grad_sum_rows >= 1, "drpo_optim_step: segment %d: grad_sum_rows", k);
     a.seg[k] = S;
     a.first[k] = tot;
     tot += (S.end - S.start + OPT_BLOCK_ELEMS - 1) / OPT_BLOCK_ELEMS;

@@ -443,6 +443,10 @@ struct PersistArgs {
   int* cnt;             // [H][ntiles] rows alive at the start of step t
   int* inv;             // [H][ntiles*ROWS] in-tile index of the k-th alive row
   int ldx, ldh, ldm, lds;
+  // small rollouts: block 0 copies the buffer pointer into base_slot before any emit
+  // (rollout_emit_self_kernel then reads the copy and advances *vptr itself)
+  const int64_t* vptr_in;
+  int64_t* base_slot;
   int members[PERSIST_MAX_H];
 };
 
@@ -498,6 +502,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int S = p.S, A = p.A, C = p.C, S1 = p.S + 1, B = p.B;
+  if (p.base_slot && blockIdx.x == 0 && tid == 0) *p.base_slot = *p.vptr_in;
 
   // LDS carve-up. Re-derived at the top of every horizon step from an opaque zero
   // and opaque leading dimensions: otherwise LICM hoists every (loop-invariant)
@@ -827,7 +832,68 @@ __global__ __launch_bounds__(256) void rollout_emit_kernel(PersistArgs p, const 
   vv[q] = (dv >> 1) & 1;
 }
 
-// Small rollouts (H x tiles <= 16384 counts): the per-step scans, the step offsets and
+// Small rollouts (H x tiles <= EMIT_SELF_MAX counts): count scan, ordered emit and
+// pointer advance in ONE launch. Every workgroup reads the whole [H][ntiles] count
+// array (<= 32 KB, L2-resident: the persist kernel just wrote it) and reduces it to
+// its own flat prefix (all rows of steps < t, and of tiles before its first tile at
+// step t) and the total, so no workgroup waits on another. The buffer pointer was
+// copied into base_slot by rollout_persist_kernel, so the one workgroup that advances
+// *vptr races with no reader.
+constexpr int EMIT_SELF_MAX = 8192;
+template <int ROWS>
+__global__ __launch_bounds__(256) void rollout_emit_self_kernel(PersistArgs p, const int64_t* __restrict__ base_slot,
+                                                                int64_t* __restrict__ vptr, int64_t* __restrict__ off,
+                                                                int64_t vcap, float* __restrict__ vs,
+                                                                float* __restrict__ va, float* __restrict__ vs2,
+                                                                float* __restrict__ vr, float* __restrict__ vh,
+                                                                uint8_t* __restrict__ vd, uint8_t* __restrict__ vv) {
+  constexpr int TPB = 256 / ROWS;   // tiles per workgroup
+  __shared__ int s_pre[4], s_tot[4], s_loc[TPB];
+  const int t = blockIdx.y, tid = threadIdx.x;
+  const int tile0 = blockIdx.x * TPB;
+  const int nflat = p.H * p.ntiles, P = t * p.ntiles + tile0;
+  const int* __restrict__ cnt = p.cnt;
+  int pre = 0, tot = 0;
+  for (int i = tid; i < nflat; i += 256) {
+    const int c = cnt[i];
+    tot += c;
+    pre += i < P ? c : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    pre += __shfl_xor(pre, o, 64);
+    tot += __shfl_xor(tot, o, 64);
+  }
+  if ((tid & 63) == 0) { s_pre[tid >> 6] = pre; s_tot[tid >> 6] = tot; }
+  if (tid < TPB) s_loc[tid] = tile0 + tid < p.ntiles ? cnt[(size_t)t * p.ntiles + tile0 + tid] : 0;
+  __syncthreads();
+  pre = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+  tot = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+  const int64_t base = *base_slot;
+  if (t == p.H - 1 && blockIdx.x == gridDim.x - 1 && tid == 0) {
+    off[p.H] = tot;
+    *vptr = base + tot;
+  }
+  const int j = tid / ROWS, k = tid - j * ROWS, tile = tile0 + j;
+  if (tile >= p.ntiles || k >= s_loc[j]) return;
+  int loc = 0;
+  for (int u = 0; u < j; ++u) loc += s_loc[u];
+  const int S = p.S, A = p.A, C = p.C;
+  const size_t ti = (size_t)t * p.ntiles + tile;
+  const size_t src = (size_t)t * p.B + (size_t)tile * ROWS + p.inv[ti * ROWS + k];
+  const int64_t q = (base + pre + loc + k) % vcap;
+  for (int jj = 0; jj < S; ++jj) {
+    vs[q * S + jj] = p.st_s[src * S + jj];
+    vs2[q * S + jj] = p.st_s2[src * S + jj];
+  }
+  for (int d = 0; d < A; ++d) va[q * A + d] = p.st_a[src * A + d];
+  for (int c = 0; c < C; ++c) vh[q * C + c] = p.st_h[src * C + c];
+  vr[q] = p.st_r[src];
+  const uint8_t dv = p.st_dv[src];
+  vd[q] = dv & 1;
+  vv[q] = (dv >> 1) & 1;
+}
+
+// Mid-size rollouts (H x tiles <= 16384 counts): the per-step scans, the step offsets and
 // the pointer advance of rollout_scan_kernel + rollout_persist_finalize_kernel in ONE
 // single-workgroup launch (the emit then reads the advanced pointer minus the total).
 __global__ __launch_bounds__(256) void rollout_scanfin_kernel(const int* __restrict__ cnt, int* __restrict__ pos,
@@ -906,7 +972,7 @@ static size_t rollout_ws_offsets(int B, int S, int H, size_t off[WS_PIECES]) {
   const size_t bytes[WS_PIECES] = {sizeof(float) * (size_t)B * S, sizeof(float) * (size_t)B * S,
                                    sizeof(int) * T16, sizeof(int) * T16,
                                    sizeof(int) * (size_t)B, sizeof(int) * (size_t)B,
-                                   sizeof(int) * (size_t)(H + 1), sizeof(int64_t) * (size_t)(H + 1),
+                                   sizeof(int) * (size_t)(H + 1), sizeof(int64_t) * (size_t)(H + 2),
                                    sizeof(float) * HB * S, sizeof(float) * HB * S, sizeof(float) * HB * 8,
                                    sizeof(float) * HB, sizeof(float) * HB * 8, HB,
                                    sizeof(int) * (size_t)H * T16, sizeof(int) * (size_t)H * (B + 32),
@@ -1010,6 +1076,12 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   const size_t lw_bytes = sizeof(float) * (size_t)(32 + 16 * PERSIST_L2_LDS) * 256;
   const bool lw = rpt == 16 && NW == 8 && S <= 16 && d->Ha == 256 && 2 * A <= 16 && lds_bytes + lw_bytes <= 160 * 1024 &&
                   !getenv("DRPO_ROLLOUT_NO_LDS_WEIGHTS");
+  static const bool scan_emit = getenv("DRPO_ROLLOUT_SCAN_EMIT") != nullptr;   // A/B: the two-launch tail
+  const bool self_emit = (int64_t)H * a.ntiles <= EMIT_SELF_MAX && !scan_emit;
+  if (self_emit) {
+    a.vptr_in = d->vptr;
+    a.base_slot = off + H + 1;
+  }
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
   if (rpt == 32)
     rollout_persist_kernel<2, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
@@ -1021,7 +1093,18 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
     rollout_persist_kernel<1, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   DRPO_LAUNCH_CHECK("rollout_persist");
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[1], stream);
-  // small rollouts: scan + offsets + pointer advance in one single-workgroup launch
+  const dim3 eg((unsigned)((a.ntiles * rpt + 255) / 256), (unsigned)H);
+  if (self_emit) {
+    if (rpt == 32)
+      rollout_emit_self_kernel<32><<<eg, 256, 0, stream>>>(a, off + H + 1, d->vptr, off, d->vcap, d->vs, d->va,
+                                                           d->vs2, d->vr, d->vh, d->vd, d->vv);
+    else
+      rollout_emit_self_kernel<16><<<eg, 256, 0, stream>>>(a, off + H + 1, d->vptr, off, d->vcap, d->vs, d->va,
+                                                           d->vs2, d->vr, d->vh, d->vd, d->vv);
+    DRPO_LAUNCH_CHECK("rollout_emit_self");
+    return DRPO_OK;
+  }
+  // mid-size rollouts: scan + offsets + pointer advance in one single-workgroup launch
   const int fin1 = (int64_t)H * a.ntiles <= 16384;
   if (fin1) {
     rollout_scanfin_kernel<<<1, 256, 0, stream>>>(a.cnt, pos, n, off, d->vptr, a.ntiles, H);
@@ -1030,7 +1113,6 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
     rollout_scan_kernel<<<H, 256, 0, stream>>>(a.cnt, pos, n, a.ntiles);
     DRPO_LAUNCH_CHECK("rollout_scan");
   }
-  const dim3 eg((unsigned)((a.ntiles * rpt + 255) / 256), (unsigned)H);
   if (rpt == 32)
     rollout_emit_kernel<32><<<eg, 256, 0, stream>>>(a, pos, n, d->vptr, fin1, off, d->vcap, d->vs, d->va,
                                                     d->vs2, d->vr, d->vh, d->vd, d->vv);

@@ -234,8 +234,6 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
     const float e0 = p.q0[i] - y, e1 = p.q1[i] - y;
     const float invB = 1.f / (float)p.B;
     lq = (e0 * e0 + e1 * e1) * (0.5f * invB);
-    p.dq0[i] = e0 * invB;
-    p.dq1[i] = e1 * invB;
     const float invN = 1.f / (float)(p.B * p.C);
     for (int c = 0; c < p.C; ++c) {
       const int64_t k = i * p.C + c;
@@ -267,6 +265,10 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
         if (p.dls) p.dls[k] = 0.f;
       }
     }
+    // the critic gradients are stored after the certificate loop: a store ahead of
+    // the loop's loads would cost the row a second memory latency
+    p.dq0[i] = e0 * invB;
+    p.dq1[i] = e1 * invB;
   }
   const float s0 = block_sum(lq, red);
   const float s1 = block_sum(lc, red);
@@ -294,37 +296,50 @@ DRPO_API int drpo_critic_head(const drpo_critic_head_t* p, drpo_stream_t stream_
 __global__ void actor_upstream_kernel(int64_t B, int C, int dist, float ratio, float lmin, float lmax,
                                       const float* lams, const float* mu_a, const float* ls_a, const float* mu_s,
                                       const float* ls_s, float* gq, float* gmu_a, float* gls_a, float* gmu_s,
-                                      float* gls_s) {
+                                      float* gls_s, float ub) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const float invB = 1.f / (float)B;
-  if (gq) gq[i] = -invB;
+  // pass 1, loads only: the arg-max constraint of each side and its raw log-std (both
+  // sides' loads are in flight together; no store sits between them)
+  int bis[2] = {0, 0};
+  float lsb[2] = {0.f, 0.f};
+  float lam = gmu_a ? lams[i] : 0.f;
+  if (ub > 0.f) lam = ub / 2.f * (1.f + tanhf(lam / ub * 2.f));   // MLPMultiplier.forward transform
+#pragma unroll
   for (int side = 0; side < 2; ++side) {
     const float* mu = side ? mu_s : mu_a;
     const float* ls = side ? ls_s : ls_a;
-    float* gmu = side ? gmu_s : gmu_a;
-    float* gls = side ? gls_s : gls_a;
-    if (!gmu) continue;
-    const float g = side ? invB : lams[i] * invB;
-    float best = 0.f;
+    if (!(side ? gmu_s : gmu_a)) continue;
+    float best = 0.f, lbest = 0.f;
     int bi = 0;
     for (int c = 0; c < C; ++c) {
       float v = mu[i * C + c];
-      if (dist) v = v + ratio * cc_std(ls[i * C + c], lmin, lmax);
-      if (c == 0 || v > best) { best = v; bi = c; }
+      const float l = dist ? ls[i * C + c] : 0.f;
+      if (dist) v = v + ratio * cc_std(l, lmin, lmax);
+      if (c == 0 || v > best) { best = v; bi = c; lbest = l; }
+    }
+    bis[side] = bi;
+    lsb[side] = lbest;
+  }
+  // pass 2, stores
+  if (gq) gq[i] = -invB;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    float* gmu = side ? gmu_s : gmu_a;
+    float* gls = side ? gls_s : gls_a;
+    if (!gmu) continue;
+    const float g = side ? invB : lam * invB;
+    float gl = 0.f;
+    if (dist && g != 0.f) {
+      const float sd = cc_std(lsb[side], lmin, lmax);
+      gl = g * ratio * cc_dstd_draw(lsb[side], lmin, lmax, sd);
     }
     for (int c = 0; c < C; ++c) {
       const int64_t k = i * C + c;
-      const float gc = (c == bi) ? g : 0.f;
-      gmu[k] = gc;
-      if (gls) {
-        if (dist && gc != 0.f) {
-          const float sd = cc_std(ls[k], lmin, lmax);
-          gls[k] = gc * ratio * cc_dstd_draw(ls[k], lmin, lmax, sd);
-        } else {
-          gls[k] = 0.f;
-        }
-      }
+      const bool hit = c == bis[side];
+      gmu[k] = hit ? g : 0.f;
+      if (gls) gls[k] = hit ? gl : 0.f;
     }
   }
 }
@@ -332,12 +347,12 @@ __global__ void actor_upstream_kernel(int64_t B, int C, int dist, float ratio, f
 DRPO_API int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, float log_std_min,
                                  float log_std_max, const float* lams, const float* mu_a, const float* ls_a,
                                  const float* mu_s, const float* ls_s, float* gq, float* gmu_a, float* gls_a,
-                                 float* gmu_s, float* gls_s, drpo_stream_t stream_) {
+                                 float* gmu_s, float* gls_s, float lam_upper_bound, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   actor_upstream_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(
       B, C, distributional, std_ratio, log_std_min, log_std_max, lams, mu_a, ls_a, mu_s, ls_s, gq, gmu_a, gls_a,
-      gmu_s, gls_s);
+      gmu_s, gls_s, lam_upper_bound);
   DRPO_LAUNCH_CHECK("actor_upstream");
   return DRPO_OK;
 }
@@ -349,6 +364,7 @@ DRPO_API int drpo_actor_upstream(int64_t B, int C, int distributional, float std
 // actor, read as alpha = exp(*log_alpha) * lp_scale when log_alpha != NULL).
 // Writes draw [B][2A] = dL/d(mu, raw log-std). Optionally accumulates
 // sum_i (logp_i + target_entropy) into *alpha_sum (alpha loss).
+constexpr int SQ_MAXA = 8;   // action width bound of the row-wise heads
 __global__ __launch_bounds__(256) void squash_bwd_kernel(int64_t B, int A, const float* raw, const float* u,
                                                          const float* e, const float* dA, const float* dA2, const float* log_alpha,
                                                          float lp_scale, const float* logp, float target_entropy,
@@ -357,23 +373,35 @@ __global__ __launch_bounds__(256) void squash_bwd_kernel(int64_t B, int A, const
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float acc = 0.f;
   if (i < B) {
+    // every load of the row is issued before the first store (a store between two
+    // dependent load groups costs a second memory latency per row)
+    float mu[SQ_MAXA], rr[SQ_MAXA], uu[SQ_MAXA], ee[SQ_MAXA], dAv[SQ_MAXA];
+#pragma unroll
+    for (int d = 0; d < SQ_MAXA; ++d) {
+      if (d >= A) break;
+      mu[d] = raw[i * 2 * A + d];
+      rr[d] = raw[i * 2 * A + A + d];
+      uu[d] = u[i * A + d];
+      ee[d] = e[i * A + d];
+      dAv[d] = dA2 ? dA[i * A + d] + dA2[i * A + d] : dA[i * A + d];
+    }
+    const float lpi = alpha_sum ? logp[i] : 0.f;
     const float glp = log_alpha ? expf(*log_alpha) * lp_scale : 0.f;
-    for (int d = 0; d < A; ++d) {
-      const float mu = raw[i * 2 * A + d], r = raw[i * 2 * A + A + d];
-      const float sg = sigmoidf(r);
+#pragma unroll
+    for (int d = 0; d < SQ_MAXA; ++d) {
+      if (d >= A) break;
+      const float sg = sigmoidf(rr[d]);
       const float sd = expf(-6.f + 10.f * sg) * 1.0f;
-      const float uu = u[i * A + d], ee = e[i * A + d];
-      const float a = tanhf(uu);
-      const float diff = uu - mu;
+      const float a = tanhf(uu[d]);
+      const float diff = uu[d] - mu[d];
       const float var = sd * sd;
-      const float dAv = dA2 ? dA[i * A + d] + dA2[i * A + d] : dA[i * A + d];
-      const float du = dAv * (1.f - a * a) + glp * (-diff / var + 2.f - 4.f * sp_grad(-2.f * uu));
+      const float du = dAv[d] * (1.f - a * a) + glp * (-diff / var + 2.f - 4.f * sp_grad(-2.f * uu[d]));
       const float dmu = du + glp * diff / var;
-      const float dsd = du * ee + glp * (diff * diff / (var * sd) - 1.f / sd);
+      const float dsd = du * ee[d] + glp * (diff * diff / (var * sd) - 1.f / sd);
       draw[i * 2 * A + d] = dmu;
       draw[i * 2 * A + A + d] = dsd * sd * 10.f * sg * (1.f - sg);
     }
-    if (alpha_sum) acc = logp[i] + target_entropy;
+    if (alpha_sum) acc = lpi + target_entropy;
   }
   if (alpha_sum) {
     const float s = block_sum(acc, red);
@@ -385,6 +413,7 @@ DRPO_API int drpo_squash_backward(int64_t B, int A, const float* raw, const floa
                                   const float* log_alpha, float lp_scale, const float* logp, float target_entropy,
                                   float* alpha_sum, float* draw, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(A >= 1 && A <= SQ_MAXA, "drpo_squash_backward: action width %d", A);
   if (B == 0) return DRPO_OK;
   squash_bwd_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(B, A, raw, u, e, dA, dA2, log_alpha, lp_scale, logp,
                                                                      target_entropy, alpha_sum, draw);

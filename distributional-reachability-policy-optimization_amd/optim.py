@@ -66,10 +66,12 @@ class Adam:
         if self.group is not None:
             self.group.mark_dirty()
 
-    def segment(self, start, end, scalars, clip=None, zero_grad=False, ema=None, pack_map=None, grad=None):
+    def segment(self, start, end, scalars, clip=None, zero_grad=False, ema=None, pack_map=None, grad=None,
+                grad_from_sum=None):
         """drpo_optim_seg_t for elements [start, end) of this optimizer's tensor:
         clip = (partials, max_norm); ema = (target flat tensor, rate); pack_map = device
-        drpo_pack_map_t of the group (refreshes its packed mirrors)."""
+        drpo_pack_map_t of the group (refreshes its packed mirrors); grad_from_sum =
+        (device scalar sum, rows): gradient -exp(p) * sum / rows (the SAC temperature)."""
         from ._abi import OptimSeg
         self._ensure_state()
         d = self._data()
@@ -86,6 +88,8 @@ class Adam:
         if ema is not None:
             sg.ema_target, sg.ema_rate, sg.ema_keep = ema[0].data_ptr(), float(ema[1]), float(1.0 - float(ema[1]))
         sg.map = 0 if pack_map is None else pack_map.data_ptr()
+        if grad_from_sum is not None:
+            sg.grad_from_sum, sg.grad_sum_rows = grad_from_sum[0].data_ptr(), int(grad_from_sum[1])
         return sg
 
     def step(self):

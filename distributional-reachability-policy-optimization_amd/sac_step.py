@@ -567,17 +567,18 @@ class SACEngine:
         self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
         self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
                                                  [(self.bs, S), (sqc, 1), (None, 0)], B))
-        lams = self.buf('a.lams', B)
-        _lib.check(L.drpo_multiplier_out(B, ws['a.multx'].data_ptr(), float(sol.mlp_multiplier_cfg.upper_bound),
-                                         lams.data_ptr(), _lib.stream()), 'multiplier_out')
-        # upstream gradients
+        # upstream gradients; lam = MLPMultiplier's output transform of 'a.multx', applied
+        # inside actor_upstream (no separate multiplier_out launch)
         ca, cs = self._cc_views('a.cc'), self._cc_views('a.cc2')
         gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
                                     self.buf('a.gmu2', B, C), self.buf('a.gls2', B, C))
+        ub = float(sol.mlp_multiplier_cfg.upper_bound)
+        assert ub > 0, 'MLPMultiplier upper_bound must be positive'
         _lib.check(L.drpo_actor_upstream(B, C, int(dist), float(cc.std_ratio), float(cc.log_std_min),
-                                         float(cc.log_std_max), lams.data_ptr(), ca[0].data_ptr(), ca[1].data_ptr(),
-                                         cs[0].data_ptr(), cs[1].data_ptr(), gq.data_ptr(), gmu.data_ptr(),
-                                         gls.data_ptr(), gmu2.data_ptr(), gls2.data_ptr(), _lib.stream()),
+                                         float(cc.log_std_max), ws['a.multx'].data_ptr(), ca[0].data_ptr(),
+                                         ca[1].data_ptr(), cs[0].data_ptr(), cs[1].data_ptr(), gq.data_ptr(),
+                                         gmu.data_ptr(), gls.data_ptr(), gmu2.data_ptr(), gls2.data_ptr(), ub,
+                                         _lib.stream()),
                    'actor_upstream')
         # dL/da of the actor (Q_k part + certificate part, summed in squash_backward in
         # the reference's order) and of the safe actor: one backward launch
@@ -605,10 +606,12 @@ class SACEngine:
         na, ns = n['actor'], n['safe']
         self._run_wgrad('a.wg', lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]]), (ns, [xs, ns.sy[0], ns.sy[1]])],
                                                     B))
+        # d alpha_loss / d log_alpha = -exp(log_alpha) * mean(logp + target_entropy) is formed
+        # inside the optimizer launch from the alpha-loss sum (src/ssac.py:498-501); under
+        # DP the sum is mean-reduced instead of the gradient (same value: log_alpha is
+        # replicated)
         ag = self.buf('a.alpha_grad', 1)
-        _lib.check(L.drpo_alpha_grad(sol.log_alpha.data_ptr(), asum.data_ptr(), B, ag.data_ptr(), _lib.stream()),
-                   'alpha_grad')
-        self.dp.mean_(sol.actor.group.grad, sol.actor_safe.group.grad, ag)
+        self.dp.mean_(sol.actor.group.grad, sol.actor_safe.group.grad, asum)
         # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam +
         # cosine -- one sum-of-squares launch and one fused optimizer launch
         ga, gs = sol.actor.group, sol.actor_safe.group
@@ -621,7 +624,7 @@ class SACEngine:
             aopt.tensor = sol.log_alpha.view(1)
         segs = [sol.actor_optimizer.segment(0, ga.size, sol.actor_optimizer.step_scalars(), clip=(pa, sol.grad_norm),
                                             zero_grad=True, pack_map=ga.pack_map()),
-                aopt.segment(0, 1, aopt.step_scalars(), grad=ag),
+                aopt.segment(0, 1, aopt.step_scalars(), grad=ag, grad_from_sum=(asum, B)),
                 sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
                                                  clip=(ps, sol.grad_norm), zero_grad=True, pack_map=gs.pack_map())]
         fused_step(segs)

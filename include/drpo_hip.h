@@ -302,7 +302,11 @@ int drpo_critic_head(const drpo_critic_head_t* p /* host */, drpo_stream_t strea
 /* dL/d outputs of the critic and constraint critic for actor_loss (src/ssac.py:458-505) */
 int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, float log_std_min, float log_std_max,
                         const float* lams, const float* mu_a, const float* ls_a, const float* mu_s, const float* ls_s,
-                        float* gq, float* gmu_a, float* gls_a, float* gmu_s, float* gls_s, drpo_stream_t stream);
+                        float* gq, float* gmu_a, float* gls_a, float* gmu_s, float* gls_s,
+                        float lam_upper_bound /* > 0: lams holds the MLPMultiplier's raw output x and
+                                                 lam = ub/2 (1 + tanh(2x/ub)) (src/ssac.py:107-111) is
+                                                 applied here; 0: lams holds lam */,
+                        drpo_stream_t stream);
 
 /* chain rule through rsample/tanh/log_prob to the actor head; alpha-loss sum */
 int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, const float* e, const float* dA,
@@ -386,6 +390,12 @@ typedef struct {
   float* ema_target;          /* optional: target = rate*p + keep*target */
   float ema_rate, ema_keep;
   const drpo_pack_map_t* map; /* optional (device): packed mirrors to refresh */
+  const float* grad_from_sum; /* optional (device scalar): the gradient of element i is
+                                 -exp(p_i) * (*grad_from_sum / grad_sum_rows) instead of g[i]:
+                                 d alpha_loss / d log_alpha from the alpha-loss sum of
+                                 drpo_squash_backward (src/ssac.py:498-501), so the SAC
+                                 temperature needs no separate gradient launch */
+  int64_t grad_sum_rows;
 } drpo_optim_seg_t;
 
 int drpo_optim_step(const drpo_optim_seg_t* segs /* host, <= 8 */, int n, drpo_stream_t stream);
