@@ -87,6 +87,8 @@ PROTOTYPES = {
     'drpo_pack_weights': (c_int, [POINTER(PackItem), c_int, P]),
     'drpo_ens_gather': (c_int, [P, P, P, P, c_int64, P, c_int64, c_int64, P, c_uint64, c_uint64, c_int, c_int, P, P,
                                 P, P]),
+    'drpo_ens_gather_steps': (c_int, [P, P, P, P, c_int64, P, c_int64, c_int64, c_int64, P, c_uint64, c_uint64,
+                                      c_int, c_int, P, P, P, P]),
     'drpo_ens_head': (c_int, [P, P, P, c_int64, c_int64, c_int, c_int, P, P, P, P, c_uint64, c_uint64, P, P, P, P,
                               P]),
     'drpo_ens_loss_workspace_size': (c_size_t, [c_int64, c_int, c_int]),

@@ -46,53 +46,69 @@ __device__ __forceinline__ int64_t chrono_to_phys(int64_t j, int64_t ptr, int64_
 // threads (instead of one thread per row walking its 2S+A+1 columns) keeps the whole
 // chip's memory pipes busy. Each thread derives its row's index itself (recorded,
 // or the row's Philox draw -- the same value for every column of the row).
+// steps > 1: the minibatches of `steps` consecutive fit steps in ONE launch (step k:
+// rows [k*rows, (k+1)*rows) of every output, indices idx[k*rows ..] or Philox counter
+// ctr + k), so the fit loop pays one latency-bound gather per chunk of steps instead
+// of one per step (the replay is not written during a fit).
 __global__ void ens_gather_kernel(const float* __restrict__ bs, const float* __restrict__ ba,
                                   const float* __restrict__ bs2, const float* __restrict__ br, int64_t ptr,
-                                  const int64_t* ptr_dev, int64_t cap, int64_t rows, const int64_t* idx,
-                                  uint64_t seed, uint64_t ctr, int S, int A, float* __restrict__ xs,
-                                  float* __restrict__ xa, float* __restrict__ xt) {
+                                  const int64_t* ptr_dev, int64_t cap, int64_t rows, int64_t steps,
+                                  const int64_t* idx, uint64_t seed, uint64_t ctr, int S, int A,
+                                  float* __restrict__ xs, float* __restrict__ xa, float* __restrict__ xt) {
   const int W = 2 * S + A + 1;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= rows * W) return;
-  const int64_t i = e / W;
-  const int c = (int)(e - i * W);
+  if (e >= steps * rows * W) return;
+  const int64_t gi = e / W;                  // row over all steps
+  const int c = (int)(e - gi * W);
+  const int64_t st = gi / rows, i = gi - st * rows;
   const int64_t p = ptr_dev ? *ptr_dev : ptr;
   const int64_t n = p < cap ? p : cap;
   int64_t j;
   if (idx) {
-    j = idx[i];
+    j = idx[gi];
   } else {
-    const u32x4 r = philox({(uint32_t)i, (uint32_t)(i >> 32), 0xe5e3b1u, (uint32_t)ctr}, (uint32_t)seed,
+    const uint64_t cs = ctr + (uint64_t)st;
+    const u32x4 r = philox({(uint32_t)i, (uint32_t)(i >> 32), 0xe5e3b1u, (uint32_t)cs}, (uint32_t)seed,
                            (uint32_t)(seed >> 32));
     j = (int64_t)((((uint64_t)r.y << 32) | r.x) % (uint64_t)n);
   }
   const int64_t q = chrono_to_phys(j, p, cap);
   if (c < S) {
-    xs[i * S + c] = bs[q * S + c];
+    xs[gi * S + c] = bs[q * S + c];
   } else if (c < S + A) {
-    xa[i * A + (c - S)] = ba[q * A + (c - S)];
+    xa[gi * A + (c - S)] = ba[q * A + (c - S)];
   } else if (c < 2 * S + A) {
-    xt[i * (S + 1) + (c - S - A)] = bs2[q * S + (c - S - A)];
+    xt[gi * (S + 1) + (c - S - A)] = bs2[q * S + (c - S - A)];
   } else {
-    xt[i * (S + 1) + S] = br[q];
+    xt[gi * (S + 1) + S] = br[q];
   }
+}
+
+DRPO_API int drpo_ens_gather_steps(const float* states, const float* actions, const float* next_states,
+                                   const float* rewards, int64_t ptr, const int64_t* ptr_dev, int64_t cap,
+                                   int64_t rows, int64_t steps, const int64_t* idx, uint64_t seed, uint64_t ctr,
+                                   int S, int A, float* xs, float* xa, float* xt, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(states && actions && next_states && rewards && cap >= 1 && rows >= 0 && steps >= 0 && S >= 1 &&
+                   A >= 1,
+               "drpo_ens_gather: bad arguments");
+  DRPO_REQUIRE(ptr_dev || ptr >= 1, "drpo_ens_gather: empty buffer");
+  const int64_t elems = steps * rows * (2 * S + A + 1);
+  if (elems == 0) return DRPO_OK;
+  DRPO_REQUIRE((elems + 255) / 256 <= 0x7fffffff, "drpo_ens_gather: %lld elements", (long long)elems);
+  ens_gather_kernel<<<(unsigned)((elems + 255) / 256), 256, 0, stream>>>(states, actions, next_states, rewards, ptr,
+                                                                         ptr_dev, cap, rows, steps, idx, seed, ctr,
+                                                                         S, A, xs, xa, xt);
+  DRPO_LAUNCH_CHECK("ens_gather");
+  return DRPO_OK;
 }
 
 DRPO_API int drpo_ens_gather(const float* states, const float* actions, const float* next_states,
                              const float* rewards, int64_t ptr, const int64_t* ptr_dev, int64_t cap, int64_t rows,
                              const int64_t* idx, uint64_t seed, uint64_t ctr, int S, int A, float* xs, float* xa,
-                             float* xt, drpo_stream_t stream_) {
-  hipStream_t stream = (hipStream_t)stream_;
-  DRPO_REQUIRE(states && actions && next_states && rewards && cap >= 1 && rows >= 0 && S >= 1 && A >= 1,
-               "drpo_ens_gather: bad arguments");
-  DRPO_REQUIRE(ptr_dev || ptr >= 1, "drpo_ens_gather: empty buffer");
-  if (rows == 0) return DRPO_OK;
-  const int64_t elems = rows * (2 * S + A + 1);
-  ens_gather_kernel<<<(unsigned)((elems + 255) / 256), 256, 0, stream>>>(states, actions, next_states, rewards, ptr,
-                                                                         ptr_dev, cap, rows, idx, seed, ctr, S, A,
-                                                                         xs, xa, xt);
-  DRPO_LAUNCH_CHECK("ens_gather");
-  return DRPO_OK;
+                             float* xt, drpo_stream_t stream) {
+  return drpo_ens_gather_steps(states, actions, next_states, rewards, ptr, ptr_dev, cap, rows, 1, idx, seed, ctr, S,
+                               A, xs, xa, xt, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -354,14 +354,29 @@ class EnsembleEngine:
         stream = _lib.stream()
         gargs = [_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states), _lib.ptr(rb._rewards),
                  ptr_host, _lib.ptr(ptr_dev), rb.capacity, rows]
-        gouts = [S, A, _lib.ptr(xs), _lib.ptr(xa), _lib.ptr(xt), stream]
         loss_base = losses.data_ptr()
+        # The minibatches of a chunk of steps are gathered in ONE launch (the replay is
+        # not written during the fit); the step's forward / loss descriptors are pointed
+        # at its slice. Chunks of <= 64 MB of gathered rows.
+        W = 2 * S + A + 1
+        chunk = max(1, min(steps, (64 << 20) // (4 * W * max(rows, 1))))
+        cs, ca, ct = (self.buf('fit.s_all', chunk * rows, S), self.buf('fit.a_all', chunk * rows, A),
+                      self.buf('fit.t_all', chunk * rows, S1))
         for i in range(steps):
-            if idx_all is not None:
-                idx, ctr = ctypes.c_void_p(idx_all.data_ptr() + 8 * rows * i), 0
-            else:
-                idx, ctr = None, nz.next()
-            _lib.check(L.drpo_ens_gather(*gargs, idx, nz.seed, ctr, *gouts), 'ens_gather')
+            k = i % chunk
+            if k == 0:
+                nc = min(chunk, steps - i)
+                if idx_all is not None:
+                    idx, ctr = ctypes.c_void_p(idx_all.data_ptr() + 8 * rows * i), 0
+                else:   # the counters the per-step draws would take: ctr, ctr + 1, ...
+                    idx, ctr = None, nz.next()
+                    for _ in range(nc - 1):
+                        nz.next()
+                _lib.check(L.drpo_ens_gather_steps(*gargs, nc, idx, nz.seed, ctr, S, A, _lib.ptr(cs), _lib.ptr(ca),
+                                                   _lib.ptr(ct), stream), 'ens_gather')
+            fd.src[0], fd.src[1] = cs.data_ptr() + 4 * k * rows * S, ca.data_ptr() + 4 * k * rows * A
+            largs[2] = ctypes.c_void_p(fd.src[0])
+            largs[4] = ctypes.c_void_p(ct.data_ptr() + 4 * k * rows * S1)
             _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
             largs[14] = ctypes.c_void_p(loss_base + 4 * i)
             # the loss reduction rides as the last workgroup of the wgrad launch

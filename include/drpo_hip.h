@@ -331,6 +331,12 @@ int drpo_multiplier_out(int64_t B, const float* x, float upper_bound, float* lam
 int drpo_ens_gather(const float* states, const float* actions, const float* next_states, const float* rewards,
                     int64_t ptr, const int64_t* ptr_dev, int64_t cap, int64_t rows, const int64_t* idx, uint64_t seed,
                     uint64_t ctr, int S, int A, float* xs, float* xa, float* xt, drpo_stream_t stream);
+/* the minibatches of `steps` consecutive fit steps in one launch: step k fills rows
+ * [k*rows, (k+1)*rows) of xs / xa / xt from idx[k*rows ..] (or Philox counter ctr + k) */
+int drpo_ens_gather_steps(const float* states, const float* actions, const float* next_states, const float* rewards,
+                          int64_t ptr, const int64_t* ptr_dev, int64_t cap, int64_t rows, int64_t steps,
+                          const int64_t* idx, uint64_t seed, uint64_t ctr, int S, int A, float* xs, float* xa,
+                          float* xt, drpo_stream_t stream);
 /* mu = diff + [s, 0], soft log-var clamp, optional sample -> (s', r)
  * (_forward1 / _forward_all / sample / elite_samples, src/dynamics.py:112-134,198-234) */
 int drpo_ens_head(const float* D, const float* LVR, const float* s, int64_t s_zstride, int64_t n, int S, int nz_out,
