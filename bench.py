@@ -310,7 +310,9 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--no-fit', action='store_true', help='skip the model-fit post-pass')
     ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N>1 (nccl = RCCL)')
-    ap.add_argument('--fit-steps', type=int, default=50)
+    ap.add_argument('--fit-steps', type=int, default=None,
+                    help="steps of the timed fit call (default: the config's model_steps, the length of "
+                         "the reference's fit(steps=) call, src/smbpo.py:214-216)")
     ap.add_argument('--engine', type=int, default=0, help='rollout engine: 0 auto (fused horizon), 1 per-step launches')
     args = ap.parse_args()
 
@@ -432,6 +434,8 @@ def main():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
+        if args.fit_steps is None:
+            args.fit_steps = int(getattr(alg, 'model_steps', 1000))
         f0 = time.perf_counter()
         m.fit(alg.replay_buffer, steps=args.fit_steps)   # ends with a host read of the losses
         torch.cuda.synchronize()
