@@ -497,14 +497,19 @@ def main():
     }
     if res['sac']['achieved_tflops_per_gpu'] is not None:
         res['sac']['frac'] = res['sac']['achieved_tflops_per_gpu'] / FP32_PEAK_TFLOPS
+    # HBM bytes per launch from the rocprofv3 FETCH/WRITE passes (profiles/traffic.py),
+    # attached only when those counters were taken on THIS build (same source digest)
+    from drpo_amd import _lib
     base = 'traffic_rollout_fused' if fused else 'traffic_rollout_step'
     for prof in (os.path.join(ROOT, 'profiles', f'{base}_c{args.config}.json'),
                  os.path.join(ROOT, 'profiles', f'{base}.json') if args.config == 2 else None):
         if prof and os.path.exists(prof) and not custom:
             tr = json.load(open(prof))
-            if tr.get('kernel') == kname:
+            if tr.get('kernel') == kname and tr.get('lib_digest') == _lib.build_digest():
                 res['roofline']['traffic'] = tr.get('bytes_per_launch')
+                res['roofline']['traffic_source'] = os.path.relpath(prof, ROOT)
                 break
+    res['lib_digest'] = _lib.build_digest()
     if world == 1 and not args.no_cpu_baseline:
         res['cpu_baseline'] = cpu_baseline(cfgd, args.seed)
     print(json.dumps(res))

@@ -48,7 +48,7 @@ class OptimSeg(ctypes.Structure):
                 ('lr_over_bc1', c_float), ('bc2_sqrt', c_float), ('beta1', c_float), ('beta2', c_float),
                 ('eps', c_float), ('weight_decay', c_float), ('zero_grad', c_int),
                 ('ema_target', P), ('ema_rate', c_float), ('ema_keep', c_float), ('map', P),
-                ('grad_from_sum', P), ('grad_sum_rows', c_int64)]
+                ('grad_from_sum', P), ('grad_sum_rows', c_int64), ('grad_scale', c_float)]
 
 
 class EnsReduce(ctypes.Structure):
@@ -61,6 +61,7 @@ class EnsReduce(ctypes.Structure):
 PROTOTYPES = {
     'drpo_version': (c_int, []),
     'drpo_last_error': (c_char_p, []),
+    'drpo_build_digest': (c_char_p, []),
     'drpo_abi_sizeof': (c_int64, [c_char_p]),
     'drpo_rollout_workspace_size': (c_size_t, [c_int, c_int, c_int]),
     'drpo_rollout_count_offset': (c_size_t, [c_int, c_int, c_int]),

@@ -26,10 +26,20 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise DrpoError(f'{LIB_PATH} is missing: build it with __graft_entry__.build() '
                             '(the HIP path has no CPU fallback)')
-        _lib = ctypes.CDLL(LIB_PATH)
-        from . import _abi
-        _abi.declare(_lib)
+        lib_ = ctypes.CDLL(LIB_PATH)
+        from . import _abi, build_lib
+        _abi.declare(lib_)
+        got, want = lib_.drpo_build_digest().decode(), build_lib.source_digest()
+        if got != want:
+            raise DrpoError(f'{LIB_PATH} was built from other sources (library digest {got[:16]}, '
+                            f'csrc/include digest {want[:16]}): rebuild it with __graft_entry__.build()')
+        _lib = lib_
     return _lib
+
+
+def build_digest():
+    """Source digest compiled into the loaded library (== build_lib.source_digest())."""
+    return lib().drpo_build_digest().decode()
 
 
 def check(rc, what=''):

@@ -87,6 +87,40 @@ def _headers():
     return glob.glob(os.path.join(CSRC, '*.hpp')) + glob.glob(os.path.join(HERE, '..', 'include', '*.h'))
 
 
+def source_digest():
+    """SHA-256 of every source the library is built from (csrc/*.hip, csrc/*.hpp,
+    include/*.h; names and contents). It is compiled INTO the library
+    (drpo_build_digest) and _lib.lib() refuses a library whose digest differs, so a
+    stale binary can never be tested or benched."""
+    h = hashlib.sha256()
+    files = glob.glob(os.path.join(CSRC, '*.hip')) + _headers()
+    for p in sorted(files, key=os.path.basename):
+        h.update(os.path.basename(p).encode() + b'\0')
+        with open(p, 'rb') as f:
+            h.update(f.read())
+        h.update(b'\0')
+    return h.hexdigest()
+
+
+def _digest_object(objdir, flags):
+    """A one-function object exporting drpo_build_digest() -> the source digest."""
+    dig = source_digest()
+    src = os.path.join(objdir, 'build_digest.cpp')
+    text = ('extern "C" __attribute__((visibility("default"))) const char* drpo_build_digest(void) '
+            '{ return "%s"; }\n' % dig)
+    obj = os.path.join(objdir, 'build_digest.o')
+    if not _stale(obj, dig):
+        return obj
+    with open(src, 'w') as f:
+        f.write(text)
+    r = subprocess.run(['g++', '-O2', '-fPIC', '-c', src, '-o', obj], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'digest object failed:\n{r.stderr}')
+    with open(obj + '.sha256', 'w') as f:
+        f.write(dig)
+    return obj
+
+
 def _build(flags, lib, objdir, verbose, jobs):
     os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
@@ -96,6 +130,7 @@ def _build(flags, lib, objdir, verbose, jobs):
     todo = [(s, o, d) for s, o, d in zip(srcs, objs, digs) if _stale(o, d)]
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(lambda t: _compile(t[0], t[1], flags, t[2], verbose), todo))
+    objs.append(_digest_object(objdir, flags))
     return _link(objs, lib, force=bool(todo))
 
 

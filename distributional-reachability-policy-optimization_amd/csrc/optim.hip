@@ -341,12 +341,15 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
     const int* src = reinterpret_cast<const int*>(S.map);
     for (int i = threadIdx.x; i < (int)(sizeof(drpo_pack_map_t) / 4); i += 256) s_map[i] = src[i];
   }
+  // data-parallel mean folded into the step: the partial sums are of the SUMMED
+  // gradient, so the clip norm is sqrt(sum) * scale (exact for power-of-2 ranks)
+  const float gscale = S.grad_scale != 0.f ? S.grad_scale : 1.f;
   if (S.partial && threadIdx.x < 64) {
     float s = 0.f;
     for (int i = threadIdx.x; i < S.n_partial; i += 64) s += S.partial[i];
     for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
     if (threadIdx.x == 0) {
-      const float c = S.max_norm / (sqrtf(s) + 1e-6f);
+      const float c = S.max_norm / (sqrtf(s) * gscale + 1e-6f);
       s_coef = c < 1.f ? c : 1.f;
     }
   }
@@ -358,6 +361,9 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
     const float gs = *S.grad_from_sum * (1.f / (float)S.grad_sum_rows);
 #pragma unroll
     for (int e = 0; e < 4; ++e) g[e] = -expf(p[e]) * gs;
+  } else if (gscale != 1.f) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[e] *= gscale;
   }
   if (S.adam) {
 #pragma unroll

@@ -36,6 +36,19 @@ def rank():
     return _dist.get_rank() if is_active() else 0
 
 
+def broadcast_int(value, src=0):
+    """Rank ``src``'s value of a 64-bit integer on every rank (identity when not data
+    parallel). The tensor lives where the backend exchanges: the GPU for RCCL."""
+    if not is_active():
+        return value
+    v = int(value) & 0xFFFFFFFFFFFFFFFF
+    v = v - (1 << 64) if v >= (1 << 63) else v
+    dev = torch.device('cuda', torch.cuda.current_device()) if _dist.get_backend() == 'nccl' else 'cpu'
+    t = torch.tensor([v], dtype=torch.int64, device=dev)
+    _dist.broadcast(t, src)
+    return int(t.item()) & 0xFFFFFFFFFFFFFFFF
+
+
 class GradReducer:
     """Mean all-reduce of flat gradient buffers across the data-parallel ranks."""
 
@@ -46,6 +59,21 @@ class GradReducer:
     @property
     def active(self):
         return self.world > 1
+
+    @property
+    def scale(self):
+        """1/G: the factor that turns a sum_() result into the mean. The SAC and fit
+        steps hand it to the fused optimizer (drpo_optim_seg_t.grad_scale), which
+        applies it to the gradient and to its clip norm in the same pass."""
+        return 1.0 / self.world
+
+    def sum_(self, *tensors):
+        """Sum all-reduce of flat buffers (the mean's 1/G is left to the consumer)."""
+        if self.world == 1:
+            return
+        for t in tensors:
+            if t is not None:
+                _dist.all_reduce(t, group=self.group)
 
     def mean_(self, *tensors):
         if self.world == 1:

@@ -252,8 +252,10 @@ class EnsembleEngine:
             ins = [save_x if j == 0 else trunk_out] + [net.sy[l] for l in range(len(net.layers) - 1)]
             for l, (W, bb, din, dout, act, _) in enumerate(net.layers):
                 gW, gb = net.grad_layers[l]
-                # split heads: the trunk dZ is dz + dz2, one item per term (both add into
-                # the zeroed gradient: two float adds onto 0 commute, so still deterministic)
+                # split heads: the trunk dZ is dz + dz2, one item per term, both adding
+                # into the zeroed gradient. Deterministic only while each item is ONE row
+                # chunk (rows <= the wgrad chunk, no split-K): two float adds onto 0
+                # commute, four or more addends do not. Off by default (DRPO_SPLIT_BWD).
                 for dz in (net.dz[l], net.dz2[l]):
                     if dz is None:
                         continue
@@ -306,6 +308,8 @@ class EnsembleEngine:
         m.state_normalizer.fit(rb._states[:n])
         if sh is not None:       # one normalizer for the whole ensemble (rank 0's replay)
             sh.broadcast_(m.state_normalizer.mean, m.state_normalizer.std)
+        elif self.dp.active:     # batch DP: replicas must normalise alike too
+            self.dp.broadcast_(m.state_normalizer.mean, m.state_normalizer.std)
         E, b = m.ensemble_size, m.batch_size
         z0, Z = (sh.z0, sh.count) if sh is not None else (0, E)
         rows = Z * b
@@ -328,8 +332,9 @@ class EnsembleEngine:
 
         g = m.group
         g.grad.zero_()
-        if sh is None:
-            segs = [m.optimizer.segment(0, g.size, (0.0, 1.0), zero_grad=True, pack_map=g.pack_map())]
+        if sh is None:   # batch DP: the gradient is sum-reduced, the optimizer applies 1/G
+            segs = [m.optimizer.segment(0, g.size, (0.0, 1.0), zero_grad=True, pack_map=g.pack_map(),
+                                        grad_scale=self.dp.scale)]
         else:
             ranges = self._shard_ranges(z0, Z)
             lo, hi = g.offset('min_log_var'), g.offset('max_log_var') + S1
@@ -384,7 +389,7 @@ class EnsembleEngine:
             _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
             _lib.check(L.drpo_mlp_wgrad_reduce(warr, nw, ctypes.byref(red), stream), 'ensemble wgrad')
             if sh is None:
-                self.dp.mean_(g.grad)
+                self.dp.sum_(g.grad)
             else:
                 sh.sum_(bounds_grad)      # shared log-var bounds: the sum over all members
             # Adam + grad zeroing + packed-mirror refresh in one launch

@@ -35,21 +35,39 @@ class DeviceNoise:
       the gradient of one well-defined loss.
 
     ``seed=None`` takes ``torch.initial_seed()`` (what set_seed / torch.manual_seed
-    set, src/util.py:11-17); ``rank=None`` takes the torch.distributed rank."""
+    set, src/util.py:11-17) of rank 0, broadcast to every rank when the job is data
+    parallel (a driver that seeds torch per rank, seed + rank, still gets one shared
+    host stream; constructing with seed=None is then a collective call). An explicit
+    ``seed`` must be equal on all ranks. ``rank=None`` takes the torch.distributed rank."""
     parity = False
+    COLLECT_SALT = 0xC011EC7ED
 
-    def __init__(self, seed=None, rank=None):
+    def __init__(self, seed=None, rank=None, world=None):
+        from . import distributed as dist
         if seed is None:
             import torch
-            seed = torch.initial_seed()
+            seed = dist.broadcast_int(torch.initial_seed())
         if rank is None:
-            from .distributed import rank as dist_rank
-            rank = dist_rank()
+            rank = dist.rank()
         self.base_seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.rank = int(rank)
+        self.world = dist.world_size() if world is None else int(world)
         self.seed = self.base_seed if self.rank == 0 else _mix64(self.base_seed ^ _mix64(self.rank))
         self.host = random.Random(self.base_seed)
         self.ctr = 0
+        self._collect = None
+
+    def collection(self):
+        """Noise for the real-env collection (uniform warm-up and actor actions, the
+        safety shield's critic draw; src/smbpo.py:124-136). Single process: this
+        stream. Data parallel: a stream keyed by the base seed only, identical on every
+        rank, so every replica collects the same real transitions (with identically
+        seeded envs) and fits the same normalizer and reward bounds."""
+        if self.world <= 1:
+            return self
+        if self._collect is None:
+            self._collect = DeviceNoise(_mix64(self.base_seed ^ self.COLLECT_SALT), rank=0, world=1)
+        return self._collect
 
     def next(self):
         self.ctr += 1
@@ -96,6 +114,9 @@ class TapeNoise:
 
     def next(self):
         return 0
+
+    def collection(self):
+        return self
 
     def peek(self):
         return self.entries[self.pos][0] if self.pos < len(self.entries) else None

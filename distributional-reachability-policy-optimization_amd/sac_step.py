@@ -431,10 +431,17 @@ class SACEngine:
                                 out={'s2': s2c, 'r': self.buf('c.r2m', B)})
             dm = self.buf('c.dm', B, dtype=torch.uint8)
             ep = self.env_params
-            _lib.check(L.drpo_env_constraints(ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr'],
-                                              ep['thr0'], ep['thr1'], s2c.data_ptr(), B, S,
-                                              dm.data_ptr(), self.buf('c.vm', B, dtype=torch.uint8).data_ptr(),
-                                              self.buf('c.hm', B, C).data_ptr(), _lib.stream()), 'env_constraints')
+            if ep is None:
+                # env without device constraint fns: the reference's host round trip
+                # (src/ssac.py:389, env.check_done on the model's s')
+                done_h = np.asarray(sol.env.check_done(s2c.detach().cpu().numpy())).reshape(B)
+                dm.copy_(torch.from_numpy(done_h.astype(np.uint8)))
+            else:
+                _lib.check(L.drpo_env_constraints(ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr'],
+                                                  ep['thr0'], ep['thr1'], s2c.data_ptr(), B, S,
+                                                  dm.data_ptr(), self.buf('c.vm', B, dtype=torch.uint8).data_ptr(),
+                                                  self.buf('c.hm', B, C).data_ptr(), _lib.stream()),
+                           'env_constraints')
         xs = self.buf('c.x', B, S + A)
         a2, lp2, a2s = self.buf('c.a2', B, A), self.buf('c.lp2', B), self.buf('c.a2s', B, A)
         # launch 1: a' ~ pi(s') with log pi, a'_safe ~ pi_safe(s') (robust: model s'), and
@@ -487,7 +494,7 @@ class SACEngine:
             items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]]))
         self._run_wgrad('c.wg' + str(int(dist)), lambda: wgrad_items(items, B))
         cg = sol.critic_group
-        self.dp.mean_(cg.grad)
+        self.dp.sum_(cg.grad)      # the 1/G of the mean rides in the optimizer segments
         crange = cg.span('critic.')
         ccrange = self._alive_span(cg, ['constraint_critic.trunk.', 'constraint_critic.mean_head.'] +
                                    (['constraint_critic.log_std_head.'] if dist else []))
@@ -500,7 +507,7 @@ class SACEngine:
         sc = sol.critic_optimizer.step_scalars()
         mp = cg.pack_map(tg)
         segs = [sol.critic_optimizer.segment(s0, s1, sc, clip=(pt, sol.grad_norm), zero_grad=True,
-                                             ema=(tg.data, sol.tau), pack_map=mp)
+                                             ema=(tg.data, sol.tau), pack_map=mp, grad_scale=self.dp.scale)
                 for (s0, s1), pt in zip((crange, ccrange), parts)]
         lo = 0
         for s0, s1 in sorted((crange, ccrange)) + [(cg.size, cg.size)]:
@@ -608,10 +615,11 @@ class SACEngine:
                                                     B))
         # d alpha_loss / d log_alpha = -exp(log_alpha) * mean(logp + target_entropy) is formed
         # inside the optimizer launch from the alpha-loss sum (src/ssac.py:498-501); under
-        # DP the sum is mean-reduced instead of the gradient (same value: log_alpha is
-        # replicated)
+        # DP the sum is sum-reduced and divided by G*B rows (same value: log_alpha is
+        # replicated). The actors' 1/G rides in their optimizer segments.
         ag = self.buf('a.alpha_grad', 1)
-        self.dp.mean_(sol.actor.group.grad, sol.actor_safe.group.grad, asum)
+        self.dp.sum_(sol.actor.group.grad, sol.actor_safe.group.grad, asum)
+        gsc = self.dp.scale
         # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam +
         # cosine -- one sum-of-squares launch and one fused optimizer launch
         ga, gs = sol.actor.group, sol.actor_safe.group
@@ -623,10 +631,11 @@ class SACEngine:
         if aopt.tensor is None:
             aopt.tensor = sol.log_alpha.view(1)
         segs = [sol.actor_optimizer.segment(0, ga.size, sol.actor_optimizer.step_scalars(), clip=(pa, sol.grad_norm),
-                                            zero_grad=True, pack_map=ga.pack_map()),
-                aopt.segment(0, 1, aopt.step_scalars(), grad=ag, grad_from_sum=(asum, B)),
+                                            zero_grad=True, pack_map=ga.pack_map(), grad_scale=gsc),
+                aopt.segment(0, 1, aopt.step_scalars(), grad=ag, grad_from_sum=(asum, B * self.dp.world)),
                 sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
-                                                 clip=(ps, sol.grad_norm), zero_grad=True, pack_map=gs.pack_map())]
+                                                 clip=(ps, sol.grad_norm), zero_grad=True, pack_map=gs.pack_map(),
+                                                 grad_scale=gsc)]
         fused_step(segs)
         self._grads_zeroed(ga)
         self._grads_zeroed(gs)
@@ -715,12 +724,12 @@ class SACEngine:
         nm = n['mult']
         self._run_bwd('m.bmult', lambda: fill_bwd([nm], [gx], B))
         self._run_wgrad('m.wg', lambda: wgrad_items([(nm, [xm, nm.sy[0], nm.sy[1]])], B))
-        self.dp.mean_(g.grad)
+        self.dp.sum_(g.grad)
         pm = self.buf('part.m', 4096)[:_lib.lib().drpo_grad_sumsq_blocks(g.size)]
         grad_sumsq_multi([g.grad], [pm])
         fused_step([sol.multiplier_optimizer.segment(0, g.size, sol.multiplier_optimizer.step_scalars(),
                                                      clip=(pm, sol.grad_norm), zero_grad=True,
-                                                     pack_map=g.pack_map())])
+                                                     pack_map=g.pack_map(), grad_scale=self.dp.scale)])
         self._grads_zeroed(g)
         sol.multiplier_lr_scheduler.step()
 

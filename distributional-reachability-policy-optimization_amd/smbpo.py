@@ -26,6 +26,7 @@ import torch
 from .buffers import ConstraintSafetySampleBuffer, DummyModuleWrapper
 from .checkpoint import CheckpointableData
 from .config import BaseConfig, Configurable
+from .distributed import GradReducer
 from .dynamics import BatchedGaussianEnsemble
 from .envs import ProductEnv, device_env_params, env_dims, get_max_episode_steps  # noqa: F401
 from .log import default_log as log, TabularLog
@@ -182,7 +183,7 @@ class SMBPO(Configurable, Module):
         episode = self._create_buffer(max_episode_steps)
         state = self.real_env.reset()
         while True:
-            noise = self.noise
+            noise = self.noise.collection()   # identical on every data-parallel rank
             t = int(self.steps_sampled.item())
             if t >= self.buffer_min:
                 if t % self.model_update_period == 0:
@@ -261,7 +262,10 @@ class SMBPO(Configurable, Module):
             log.message(f'\tLast {LOSS_AVERAGE_WINDOW}: {np.mean(losses[-LOSS_AVERAGE_WINDOW:])}')
             log.message(f'\tDeciles: {deciles(losses)}')
         rewards = self.replay_buffer.get('rewards')
-        self.solver.update_r_bounds(rewards.min().item() + self.alive_bonus, rewards.max().item() + self.alive_bonus)
+        bounds = torch.stack([rewards.min(), rewards.max()]).float()
+        GradReducer().broadcast_(bounds)     # data parallel: rank 0's bounds on every replica
+        r_min, r_max = bounds.tolist()
+        self.solver.update_r_bounds(r_min + self.alive_bonus, r_max + self.alive_bonus)
         return losses
 
     def update_solver(self, update_actor=True, update_multiplier=False, noise=None):

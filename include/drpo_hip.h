@@ -41,6 +41,9 @@ enum { DRPO_ENV_POINT_ROBOT = 0, DRPO_ENV_QUADROTOR = 1, DRPO_ENV_CARTPOLE = 2, 
 int drpo_version(void);
 int64_t drpo_abi_sizeof(const char* struct_name);   /* binding self-check */
 const char* drpo_last_error(void);
+/* SHA-256 (hex) of the csrc/include sources this binary was built from; the Python
+ * binding refuses a library whose digest differs from the sources beside it */
+const char* drpo_build_digest(void);
 int drpo_event_create(void** ev);
 int drpo_event_destroy(void* ev);
 int drpo_event_record(void* ev, drpo_stream_t stream);
@@ -402,6 +405,10 @@ typedef struct {
                                  drpo_squash_backward (src/ssac.py:498-501), so the SAC
                                  temperature needs no separate gradient launch */
   int64_t grad_sum_rows;
+  float grad_scale;           /* gradient multiplier applied before clip and Adam (the clip
+                                 norm is that of the scaled gradient): 1/G folds the data-
+                                 parallel mean into the step after a SUM all-reduce. 0 is
+                                 read as 1, so zero-initialised descriptors keep plain grads */
 } drpo_optim_seg_t;
 
 int drpo_optim_step(const drpo_optim_seg_t* segs /* host, <= 8 */, int n, drpo_stream_t stream);

@@ -6,6 +6,7 @@ usage: python profiles/traffic.py <fetch_counter_collection.csv> <write_counter_
 """
 import csv
 import json
+import os
 import sys
 
 
@@ -24,6 +25,12 @@ def main():
            'write_bytes': w * 1024 if w is not None else None}
     res['bytes_per_launch'] = (res['fetch_bytes'] or 0) + (res['write_bytes'] or 0)
     res['note'] = 'FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB -> bytes, mean per dispatch'
+    # the library build these counters describe (bench.py attaches the bytes only to a
+    # line measured on the same build)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    'distributional-reachability-policy-optimization_amd'))
+    import build_lib
+    res['lib_digest'] = build_lib.source_digest()
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
 

@@ -51,6 +51,9 @@ def test_host_only_entry_points(built):
     # these run without a device: version, error string, size queries
     assert built.drpo_version() >= 1
     assert isinstance(built.drpo_last_error(), bytes)
+    # the loaded binary was built from exactly the sources in the tree
+    from drpo_amd import build_lib
+    assert built.drpo_build_digest().decode() == build_lib.source_digest()
     assert built.drpo_grad_sumsq_blocks(2048 * 3 + 1) == 4
     assert built.drpo_normalizer_workspace_size(4096, 12) == 8 * 2 * 12 * 2
 
@@ -83,3 +86,12 @@ def test_struct_layouts_match(built):
     for name, cls in pairs.items():
         assert built.drpo_abi_sizeof(name.encode()) == ctypes.sizeof(cls), name
     assert built.drpo_abi_sizeof(b'nope') == -1
+
+
+def test_stale_library_is_refused(built, monkeypatch):
+    """_lib.lib() loads nothing whose compiled-in source digest differs from the tree's."""
+    from drpo_amd import build_lib
+    monkeypatch.setattr(build_lib, 'source_digest', lambda: '0' * 64)
+    monkeypatch.setattr(_lib, '_lib', None)
+    with pytest.raises(_lib.DrpoError, match='built from other sources'):
+        _lib.lib()
