@@ -333,6 +333,59 @@ __device__ __forceinline__ f32x4 load_frag(const float* __restrict__ P, const fl
   return load_pk(P, cb, s, NKS);
 }
 
+// The MFMA part of tile_dense_core for a wave owning exactly MAXC column blocks and a
+// compile-time K (NK k-steps): the accumulators and the bias values of the wave's
+// columns, for callers that fuse their own epilogue (rollout: the actor's output head
+// reduced straight from the hidden layer's accumulators).
+template <int NW, int RB, int MAXC, int NK, int NL = 0>
+__device__ __forceinline__ void tile_dense_mma(const float* in, int ldi, const float* __restrict__ P,
+                                               const float* __restrict__ bias, int N, f32x4 (&acc)[RB][MAXC],
+                                               float (&bvs)[MAXC], const float* Pl = nullptr) {
+  static_assert(NK > 0, "compile-time K only");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  int cbs[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) cbs[c] = wave + NW * c;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int PF = pf_depth<MAXC>();
+  f32x4 bq[PF][MAXC];
+#pragma unroll
+  for (int u = 0; u < PF - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) bq[u][c] = load_frag<NL>(P, Pl, cbs[c], u < NK ? u : NK - 1, NK);
+  load_bias<NW, MAXC>(bias, N, bvs);
+  f32x4 an[RB], ac[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    if (s + PF - 1 < NK) {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) bq[(s + PF - 1) % PF][c] = load_frag<NL>(P, Pl, cbs[c], s + PF - 1, NK);
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
+    if (s + 1 < NK) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 16 * (s + 1) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF][c][m], acc[rb][c], 0, 0, 0);
+  }
+}
+
 template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0>
 __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,

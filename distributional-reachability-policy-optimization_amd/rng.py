@@ -94,7 +94,11 @@ class DeviceNoise:
         return None
 
     def rand(self, shape):
-        return None
+        """Uniform [0, 1) draws of the warm-up UniformPolicy (src/policy.py:43-47): a host
+        Philox stream keyed by (seed, per-call counter) -- one action row per real step,
+        and the same on every rank for the collection stream."""
+        g = np.random.Generator(np.random.Philox(key=self.seed, counter=self.next()))
+        return g.random(shape, dtype=np.float32)
 
 
 class TapeNoise:

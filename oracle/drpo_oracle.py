@@ -263,6 +263,36 @@ def ens_fit(P, pre, opt, buf, steps, E, batch_size, holdout, num_elites, rng, lr
     return losses, elites
 
 
+def ens_fit_epochs(P, pre, opt, buf, epochs, E, batch_size, lr=1e-3):
+    """fit(epochs=...) (src/dynamics.py:185-194) -> epochal_training
+    (src/train.py:58-100): E * epochs passes of torch.randperm(n) (CPU generator)
+    minibatches of E * batch_size rows, the last ragged, one Adam step each; returns
+    the per-epoch mean losses."""
+    states, actions, next_states, rewards = buf['states'], buf['actions'], buf['next_states'], buf['rewards']
+    n = len(states)
+    P[pre + 'state_normalizer.mean'], P[pre + 'state_normalizer.std'] = normalizer_fit(states)
+    targets = torch.cat([next_states, rewards.unsqueeze(1)], dim=1)
+    keys = ens_param_keys(P, pre)
+    tb = E * batch_size
+    losses = []
+    for _ in range(E * epochs):
+        perm = torch.randperm(n)
+        ep = []
+        for bi in range(math.ceil(float(n) / tb)):
+            idx = perm[tb * bi:min(tb * (bi + 1), n)]
+            with torch.enable_grad():
+                params = {k: P[k].detach().requires_grad_(True) for k in keys}
+                Q = dict(P)
+                Q.update(params)
+                loss = ens_compute_loss(Q, pre, states[idx], actions[idx], targets[idx], E)
+                grads = torch.autograd.grad(loss, [params[k] for k in keys])
+            ep.append(loss.item())
+            for k, g in zip(keys, grads):
+                adam_update(opt, k, P[k], g.clone(), lr, 1e-4)
+        losses.append(float(np.mean(ep)))
+    return losses
+
+
 # ----------------------------------------------------------------------------
 # squashed Gaussian policy (src/policy.py:61-100, src/squashed_gaussian.py)
 # ----------------------------------------------------------------------------

@@ -114,6 +114,9 @@ def fused_stamps():
              'pair L2+gauss', 'constr+staging']
     if hm != 200:
         names[7:9] = ['diff L1+L2, lv L1', 'lv L2, gauss']
+    if hm == 200 and not os.environ.get('DRPO_ROLLOUT_V1'):     # rollout_persist2_kernel phases
+        names = ['start', 'actor L2+head', 'sample+member L1', 'member L2', 'pair L1', 'pair L2+gauss',
+                 'constr+staging+next L1']
     print('== rollout_persist_kernel step t=2 (B=4096, quadrotor): cycles per phase, mean over 256 workgroups')
     tot = 0
     for c in range(1, len(names)):

@@ -424,22 +424,41 @@ class RecordingPointRobot(PointRobot):
         return obs
 
 
-def trainer_config(seed_cfg):
-    cfg = small_config('point-robot', B=32, H=3, sac_batch=32)
+# run-ablation-1_quadrotor.sh variants (the flags main.py receives via -s):
+#   drpo         safe_shield, distributional certificate, linear evaluation shield (run.sh)
+#   vanilla      no step shield, vanilla certificate, eval_shield_type 'no' (DRPO-Vanilla, :7-17)
+#   shield_only  step shield at threshold 0.0 with the vanilla certificate, linear
+#                evaluation shield (DRPO-Shield-only, :31-41)
+#   uncert_safe  distributional certificate without the step shield (DRPO-Uncertainty-only,
+#                :19-29) evaluated with the 'safe' shield (src/sampling.py:425-428)
+TRAINER_VARIANTS = {
+    'drpo': dict(safe_shield=True, distributional=True, uncertainty=True, eval_shield_type='linear'),
+    'vanilla': dict(safe_shield=False, distributional=False, uncertainty=False, eval_shield_type='no'),
+    'shield_only': dict(safe_shield=True, distributional=False, uncertainty=False, eval_shield_type='linear'),
+    'uncert_safe': dict(safe_shield=False, distributional=True, uncertainty=True, eval_shield_type='safe'),
+}
+
+
+def trainer_config(seed_cfg, variant='drpo'):
+    v = TRAINER_VARIANTS[variant]
+    cfg = small_config('point-robot', B=32, H=3, sac_batch=32, distributional=v['distributional'],
+                       uncertainty=v['uncertainty'])
     cfg.update({'buffer_min': 40, 'steps_per_epoch': 10, 'model_update_period': 4, 'model_initial_steps': 5,
-                'model_steps': 3, 'safe_shield': True, 'safe_shield_threshold': seed_cfg['shield'],
-                'eval_shield_threshold': seed_cfg['eval_shield'], 'eval_shield_type': 'linear', 'mode': 'train'})
+                'model_steps': 3, 'safe_shield': v['safe_shield'], 'safe_shield_threshold': seed_cfg['shield'],
+                'eval_shield_threshold': seed_cfg['eval_shield'], 'eval_shield_type': v['eval_shield_type'],
+                'mode': 'train'})
     return cfg
 
 
-def gen_trainer(out, seed, shield=-0.1, eval_shield=-0.05):
+def gen_trainer(out, seed, shield=-0.1, eval_shield=-0.05, variant='drpo'):
     """main.py's loop shape (main.py:50-62): setup() -> evaluate() -> epoch() ->
     evaluate() on point-robot, with every random draw recorded. Shield decisions are
     discrete, so the generator also records how close each shield query came to its
     threshold (the parity test needs a margin well above fp32 noise)."""
     import src.ssac as ssac_mod
     from src.log import default_log as rlog
-    cfg = trainer_config({'shield': shield, 'eval_shield': eval_shield})
+    cfg = trainer_config({'shield': shield, 'eval_shield': eval_shield}, variant)
+    rlog.setup(tempfile.mkdtemp())     # a fresh run dir: episodes.csv holds this run's rows only
     RecordingPointRobot.resets = []
     set_seed(seed)
     factory = lambda id=None: TorchWrapper(RecordingPointRobot(id=id))  # noqa: E731
@@ -452,27 +471,46 @@ def gen_trainer(out, seed, shield=-0.1, eval_shield=-0.05):
     d['cfg/model_update_period'] = np.array(cfg.model_update_period)
     d['cfg/model_initial_steps'], d['cfg/model_steps'] = np.array(cfg.model_initial_steps), np.array(cfg.model_steps)
     d['cfg/shield'], d['cfg/eval_shield'] = np.array(shield), np.array(eval_shield)
+    d['cfg/variant'] = np.array(variant)
+    for k, v in TRAINER_VARIANTS[variant].items():
+        d[f'cfg/{k}'] = np.array(v)
     margins = {'step': [], 'eval': []}
     orig_get_qc = ssac_mod.SSAC._get_qc
+    in_eval = [False]
+    eval_qc = []          # per evaluation step: the performance-action query, then 11 mixes (linear)
 
     def rec_get_qc(self, q):
         out_q = orig_get_qc(self, q)
         n = out_q.reshape(-1).shape[0]
-        if n == 1:
+        if n == 1 and not in_eval[0]:
             margins['step'].append(float((out_q - shield).abs().min()))
-        elif n == 10:
-            margins['eval'].append(float((out_q - eval_shield).abs().min()))
+        elif in_eval[0]:
+            eval_qc.append(float((out_q - eval_shield).abs().min()))
         return out_q
+
+    def evaluate():
+        in_eval[0] = True
+        eval_qc.clear()
+        try:
+            ev = alg.evaluate()
+        finally:
+            in_eval[0] = False
+        # only the queries the shield type decides on (src/sampling.py:422-439)
+        etype = cfg.eval_shield_type
+        per = 12 if etype == 'linear' else 1
+        used = [m for i, m in enumerate(eval_qc) if (etype == 'linear' and i % per != 0) or etype == 'safe']
+        margins['eval'].extend(used)
+        return ev
     ssac_mod.SSAC._get_qc = rec_get_qc
     try:
         with Tape() as tp:
             alg.setup()
         d.update(tp.to_npz_dict('setup_tape'))
-        ev0 = alg.evaluate()
+        ev0 = evaluate()
         with Tape() as tp:
             alg.epoch()
         d.update(tp.to_npz_dict('epoch_tape'))
-        ev1 = alg.evaluate()
+        ev1 = evaluate()
     finally:
         ssac_mod.SSAC._get_qc = orig_get_qc
     keys = sorted(ev0)
@@ -493,10 +531,40 @@ def gen_trainer(out, seed, shield=-0.1, eval_shield=-0.05):
     for i, k in enumerate(dk):
         d[f'data/{i:03d}'] = np.array([np.nan if v is None else float(v) for v in data[k]], dtype=np.float64)
     d['episodes_csv'] = np.array(open(os.path.join(str(rlog.dir), 'episodes.csv')).read())
-    print('trainer fixture: min shield margins step %.3g eval %.3g, %d real steps, eval %s / %s' % (
-        d['margin/step'].min(), d['margin/eval'].min(), len(alg.replay_buffer), ev0, ev1))
-    np.savez_compressed(os.path.join(out, 'trainer_point-robot.npz'), **d)
+    print('trainer fixture %s seed %d: min shield margins step %.3g eval %.3g, %d real steps, eval %s / %s' % (
+        variant, seed, d['margin/step'].min(), d['margin/eval'].min(), len(alg.replay_buffer), ev0, ev1))
+    name = 'trainer_point-robot.npz' if variant == 'drpo' else f'trainer_point-robot_{variant}.npz'
+    np.savez_compressed(os.path.join(out, name), **d)
     return float(min(d['margin/step'].min(), d['margin/eval'].min()))
+
+
+# (step shield threshold, evaluation shield threshold) per variant: Shield-only runs
+# the step shield at 0.0 (run-ablation-1_quadrotor.sh:39)
+TRAINER_SHIELDS = {'shield_only': (0.0, -0.05)}
+# seeds whose shield decisions all clear their thresholds by a margin far above fp32
+# noise (printed by gen_trainer; chosen with `make_golden.py trainer <seed> <variant>`)
+TRAINER_VARIANT_SEEDS = {'vanilla': 62, 'shield_only': 63, 'uncert_safe': 64}
+
+
+def gen_fit_epochs(out, name, seed, torch_seed):
+    """fit(epochs=1) -> src/train.py::epochal_training (src/dynamics.py:185-194): E
+    epochs of torch.randperm minibatches of E*batch_size rows (the last one ragged),
+    one Adam step each. The CPU generator is re-seeded with ``torch_seed`` right before
+    the call; the build's fit_epochs draws its permutations from the same generator."""
+    cfg = small_config(name)
+    alg = build_alg(name, cfg, seed)
+    model = alg.model_ensemble
+    d = meta(name, cfg, alg)
+    d.update(sd_dict(model, 'sd/'))
+    d.update(fill_replay(alg, name, 1200, seed + 1, alg.con_dim))
+    torch.manual_seed(torch_seed)
+    d['torch_seed'] = np.array(torch_seed)
+    losses = model.fit(alg.replay_buffer, epochs=1)
+    d['out/losses'] = np.array(losses, dtype=np.float64)
+    d['model/norm_mean'] = t2n(model.state_normalizer.mean)
+    d['model/norm_std'] = t2n(model.state_normalizer.std)
+    d.update(sd_dict(model, 'fit_sd/'))
+    np.savez_compressed(os.path.join(out, f'fit_epochs_{name}.npz'), **d)
 
 
 def gen_checkpoint(out, seed):
@@ -547,7 +615,18 @@ def main():
     default_log.setup(tmp)
     if sys.argv[1:2] == ['trainer']:
         seed = int(sys.argv[2]) if len(sys.argv) > 2 else 55
-        gen_trainer(out, seed)
+        variant = sys.argv[3] if len(sys.argv) > 3 else 'drpo'
+        thr = TRAINER_SHIELDS.get(variant, (-0.1, -0.05))
+        gen_trainer(out, seed, thr[0], thr[1], variant)
+        return
+    if sys.argv[1:2] == ['variants']:
+        for variant, seed in TRAINER_VARIANT_SEEDS.items():
+            thr = TRAINER_SHIELDS.get(variant, (-0.1, -0.05))
+            gen_trainer(out, seed, thr[0], thr[1], variant)
+        return
+    if sys.argv[1:] == ['fit_epochs']:
+        gen_fit_epochs(out, 'quadrotor', 71, 17)
+        gen_fit_epochs(out, 'tracking', 72, 18)
         return
     if sys.argv[1:] == ['checkpoint']:
         gen_checkpoint(out, 61)
@@ -570,6 +649,11 @@ def main():
     gen_smbpo_update(out, 'point-robot', 41)
     gen_smbpo_update(out, 'quadrotor', 42)
     gen_trainer(out, 55)
+    for variant, seed in TRAINER_VARIANT_SEEDS.items():
+        thr = TRAINER_SHIELDS.get(variant, (-0.1, -0.05))
+        gen_trainer(out, seed, thr[0], thr[1], variant)
+    gen_fit_epochs(out, 'quadrotor', 71, 17)
+    gen_fit_epochs(out, 'tracking', 72, 18)
     gen_checkpoint(out, 61)
     print('golden fixtures written to', out)
 

@@ -10,7 +10,7 @@ DEV = torch.device('cuda')
 COMP = O.COMPONENTS
 
 
-def small_smbpo(d, env):
+def small_smbpo(d, env, factory=None):
     cfg = drpo_amd.SMBPO.Config()
     E, H, B = int(d['meta/E']), int(d['meta/H']), int(d['meta/B'])
     hid, mh = int(d['meta/hidden']), int(d['meta/model_hidden'])
@@ -25,7 +25,7 @@ def small_smbpo(d, env):
                             'distributional_qc': bool(d['meta/distributional']), 'target_entropy': -2.0,
                             'penalty_lb': -1.0, 'actor_lr': 1e-4},
                 'reward_scale': 2.0, 'alive_bonus': 2.0, 'constraint_offset': 0.5, 'constraint_scale': 10.0})
-    return drpo_amd.SMBPO(cfg, lambda id=None: ENVS[env](), None, 1, device=DEV)
+    return drpo_amd.SMBPO(cfg, factory or (lambda id=None: ENVS[env]()), None, 1, device=DEV)
 
 
 def load_sd(alg, d, prefix):

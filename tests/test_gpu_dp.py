@@ -110,3 +110,11 @@ def test_bench_two_ranks_gloo():
     res = json.loads(lines[0])
     assert res['n_gpus'] == 2 and res['value'] > 0 and res['sac']['value'] > 0
     assert res['model_fit']['sharding'].startswith('members')
+
+
+@pytest.mark.parametrize('mode', ['batch', 'members'])
+def test_dp_collection_replicas_agree(mode):
+    """step_generator past buffer_min + model fits under DP (2 ranks, gloo,
+    one GPU, torch seeded per rank): the real replay, normalizer, reward bounds,
+    elites and parameters agree on every rank; the imagined rollouts do not."""
+    _run_ranks('dp_collect_worker.py', [mode])

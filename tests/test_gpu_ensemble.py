@@ -206,6 +206,24 @@ def test_fit_epochs_vs_oracle():
         assert np.abs(got - exp).max() <= 2e-3 + 1e-2 * np.abs(exp).max(), k
 
 
+@pytest.mark.parametrize('env', ['quadrotor', 'tracking'])
+def test_fit_epochs_matches_reference_fixture(env):
+    """fit(epochs=1) against the reference's own run (src/dynamics.py:185-194 ->
+    src/train.py::epochal_training: E epochs of torch.randperm batches, the last one
+    ragged, recorded by make_golden.py with the CPU generator re-seeded right before the
+    call). Per-element parameter tolerance as the other fit tests."""
+    d = load_golden(f'fit_epochs_{env}')
+    alg, m = model_from(d, env)
+    fill(alg, d)
+    torch.manual_seed(int(d['torch_seed']))
+    losses = m.fit(alg.replay_buffer, epochs=1)
+    assert len(losses) == len(d['out/losses']) == m.ensemble_size
+    np.testing.assert_allclose(losses, d['out/losses'], rtol=1e-4)
+    close(m.state_normalizer.mean, d['model/norm_mean'], tol=1e-6, msg='normalizer mean')
+    close(m.state_normalizer.std, d['model/norm_std'], tol=1e-6, msg='normalizer std')
+    check_sd(m, d, 'fit_sd/')
+
+
 def test_fit_production_noise():
     """Device (Philox) minibatch indices: loss goes down over steps, elites are distinct
     members, parameters stay finite."""

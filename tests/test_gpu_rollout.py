@@ -254,3 +254,35 @@ def test_cartpole_threshold_follows_env():
     ref = torch.stack([-x - 0.9, -t - 0.35, x - 0.9, t - 0.35], 1)
     assert torch.equal(h, ref.float())
     assert torch.equal(viol, (ref > 0).any(1)) and torch.equal(done, viol)
+
+
+def test_rollout_host_env_fallback_matches_reference_fixture():
+    """An env class the build has no device constraint functions for (not in
+    envs.ENV_IDS) keeps the reference's host round trip (ops.rollout_host_env: HIP
+    policy + member sample, the env's own numpy check_done / check_violation /
+    get_constraint_values each step). Same reference fixture as the device path."""
+    import drpo_amd
+    from drpo_amd.envs import device_env_params
+    from pr_env import PointRobot
+
+    class HostOnlyPointRobot(PointRobot):     # unknown class name -> no device fns
+        pass
+
+    d = load_golden('rollout_point-robot')
+    alg = small_smbpo(d, 'point-robot', factory=lambda id=None: HostOnlyPointRobot())
+    assert alg.env_params is None and device_env_params(alg.real_env) is None
+    load_sd(alg, d, 'sd/')
+    fill_replay(alg, d)
+    m = alg.model_ensemble
+    m.state_normalizer.mean.copy_(torch.from_numpy(d['model/norm_mean']))
+    m.state_normalizer.std.copy_(torch.from_numpy(d['model/norm_std']))
+    m._elite_inds = list(d['model/elite_inds'])
+    tape = drpo_amd.TapeNoise.from_npz(d, 'tape')
+    alg.rollout(alg.actor, noise=tape)
+    torch.cuda.synchronize()
+    assert tape.done()
+    n = int(d['out/n'])
+    assert len(alg.virt_buffer) == n
+    got = alg.virt_buffer.get(as_dict=True)
+    for k in COMP:
+        close(got[k], d['out/' + k], msg=k)

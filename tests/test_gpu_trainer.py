@@ -32,25 +32,31 @@ DEV = torch.device('cuda')
 COMP = ('states', 'actions', 'next_states', 'rewards', 'dones', 'violations', 'constraint_values')
 
 
+def _flag(d, key, default):
+    return d[key].item() if key in d.files else default
+
+
 def _config(d):
     import drpo_amd
     cfg = drpo_amd.SMBPO.Config()
+    dist = bool(_flag(d, 'cfg/distributional', True))
+    unc = bool(_flag(d, 'cfg/uncertainty', True))
     E, H, B = int(d['meta/E']), int(d['meta/H']), int(d['meta/B'])
     hid, mh = int(d['meta/hidden']), int(d['meta/model_hidden'])
     cfg.update({'horizon': H, 'rollout_batch_size': B, 'buffer_max': int(d['meta/buffer_max']),
                 'buffer_min': int(d['cfg/buffer_min']), 'steps_per_epoch': int(d['cfg/steps_per_epoch']),
                 'model_update_period': int(d['cfg/model_update_period']),
                 'model_initial_steps': int(d['cfg/model_initial_steps']), 'model_steps': int(d['cfg/model_steps']),
-                'solver_updates_per_step': 10, 'safe_shield': True,
+                'solver_updates_per_step': 10, 'safe_shield': bool(_flag(d, 'cfg/safe_shield', True)),
                 'safe_shield_threshold': float(d['cfg/shield']), 'eval_shield_threshold': float(d['cfg/eval_shield']),
-                'eval_shield_type': 'linear', 'mode': 'train',
+                'eval_shield_type': str(_flag(d, 'cfg/eval_shield_type', 'linear')), 'mode': 'train',
                 'model_cfg': {'ensemble_size': E, 'num_elites': int(d['meta/num_elites']), 'hidden_dim': mh,
                               'batch_size': int(d['meta/model_batch']), 'holdout_size': int(d['meta/model_batch'])},
                 'sac_cfg': {'batch_size': int(d['meta/sac_batch']), 'hidden_dim': hid,
                             'critic_cfg': {'hidden_dim': hid},
                             'constraint_critic_cfg': {'hidden_dim': hid, 'std_ratio': 2.0},
                             'mlp_multiplier_cfg': {'hidden_dim': hid, 'upper_bound': 50.0},
-                            'qc_under_uncertainty': True, 'distributional_qc': True, 'target_entropy': -2.0,
+                            'qc_under_uncertainty': unc, 'distributional_qc': dist, 'target_entropy': -2.0,
                             'penalty_lb': -1.0, 'actor_lr': 1e-4},
                 'reward_scale': 2.0, 'alive_bonus': 2.0, 'constraint_offset': 0.5, 'constraint_scale': 10.0})
     return cfg
@@ -73,12 +79,20 @@ def _close(a, b, atol, rtol, msg):
         np.testing.assert_allclose(a, b, atol=atol, rtol=rtol, err_msg=msg)
 
 
-def test_setup_evaluate_epoch_matches_reference(tmp_path):
+# main.py runs: run.sh's DRPO, and run-ablation-1_quadrotor.sh's DRPO-Vanilla (no step
+# shield, vanilla certificate, eval_shield_type 'no'), DRPO-Shield-only (vanilla
+# certificate, step shield at 0.0, linear evaluation shield) and DRPO-Uncertainty-only
+# (no step shield) evaluated with the 'safe' shield
+VARIANTS = ['', '_vanilla', '_shield_only', '_uncert_safe']
+
+
+@pytest.mark.parametrize('variant', VARIANTS)
+def test_setup_evaluate_epoch_matches_reference(tmp_path, variant):
     import drpo_amd
     from drpo_amd.checkpoint import CheckpointableData
     from drpo_amd.log import default_log
     from pr_env import PointRobot, TorchEnv
-    d = load_golden('trainer_point-robot')
+    d = load_golden('trainer_point-robot' + variant)
     default_log.setup(str(tmp_path))
     resets = [np.array(r) for r in d['resets']]
     factory = lambda id=None: TorchEnv(PointRobot(id=id, resets=resets), DEV)  # noqa: E731
@@ -127,7 +141,7 @@ def test_setup_evaluate_epoch_matches_reference(tmp_path):
         np.testing.assert_allclose(got, ref, rtol=2e-3, atol=2e-3, equal_nan=True, err_msg=k)
     csv_got = open(os.path.join(str(tmp_path), 'episodes.csv')).read().splitlines()
     csv_ref = str(d['episodes_csv']).splitlines()
-    assert len(csv_got) == len(csv_ref) and csv_got[0] == csv_ref[0]
+    assert len(csv_got) == len(csv_ref) and csv_got[:1] == csv_ref[:1]
     for g, r in zip(csv_got[1:], csv_ref[1:]):
         gs, rs = g.split(','), r.split(',')
         for x, y in zip(gs, rs):

@@ -97,6 +97,26 @@ def test_ensemble_fit():
         assert_same(P[k], v, msg=k)
 
 
+@pytest.mark.parametrize('env', ['quadrotor', 'tracking'])
+def test_ensemble_fit_epochs(env):
+    """fit(epochs=1) -> epochal_training, pinned bit-exactly to the reference's run."""
+    d = load_golden(f'fit_epochs_{env}')
+    P = sd(d, 'sd/')
+    cap = int(d['meta/buffer_max'])
+    S, A, C = int(d['meta/S']), int(d['meta/A']), int(d['meta/C'])
+    buf = O.RingBuffer(S, A, C, cap)
+    rows = {k: torch.from_numpy(d['replay/' + k]) for k in O.COMPONENTS}
+    half = len(rows['states']) // 2
+    buf.extend({k: v[:half] for k, v in rows.items()})
+    buf.extend({k: v[half:] for k, v in rows.items()})
+    chrono = {k: buf.get(k) for k in O.COMPONENTS}
+    torch.manual_seed(int(d['torch_seed']))
+    losses = O.ens_fit_epochs(P, '', {}, chrono, 1, int(d['meta/E']), int(d['meta/model_batch']))
+    np.testing.assert_array_equal(np.array(losses), d['out/losses'])
+    for k, v in sd(d, 'fit_sd/').items():
+        assert_same(P[k], v, msg=k)
+
+
 @pytest.mark.parametrize('env', ['point-robot', 'quadrotor'])
 def test_rollout(env):
     d = load_golden(f'rollout_{env}')

@@ -12,14 +12,16 @@
 import io
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import load_golden
 from pr_env import PointRobot
 
 
-def test_pr_env_replays_reference_trajectory():
-    d = load_golden('trainer_point-robot')
+@pytest.mark.parametrize('variant', ['', '_vanilla', '_shield_only', '_uncert_safe'])
+def test_pr_env_replays_reference_trajectory(variant):
+    d = load_golden('trainer_point-robot' + variant)
     resets = list(d['resets'])
     env = PointRobot(resets=resets)
     S = d['replay/states']
