@@ -752,6 +752,198 @@ __device__ __forceinline__ void tile_dense_pair(const float* in, int ldi, int K,
   tile_dense_pair_nc<NW, RB, MAXC, ACT, NK, RING>(nc, in, ldi, K, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1, gs2);
 }
 
+// Two independent layers on DIFFERENT input tiles in one k-loop: column blocks
+// [0, NCB1) are in1 x P1 (N1 outputs -> out1), [NCB1, NCB1+NCB2) in2 x P2 (N2 -> out2);
+// both K = NK k-steps. Each k-step reads both inputs' A fragments and every block
+// multiplies the one of its layer (the diff and log-var output layers of the dynamics
+// model side by side; the heads of a trunk network backward together).
+template <int NW, int RB, int MAXC, int ACT, int NK, int RING = 0>
+__device__ __forceinline__ void tile_dense_pair2_core(const float* in1, const float* in2, int ldi,
+                                                      const float* __restrict__ P1, const float* __restrict__ b1,
+                                                      int N1, float* out1, const float* __restrict__ P2,
+                                                      const float* __restrict__ b2, int N2, float* out2, int ldo,
+                                                      const GSave& gs1, const GSave& gs2) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int NCB1 = (N1 + 15) >> 4, NCB2 = (N2 + 15) >> 4;
+  const float* Pc[MAXC];
+  int cbs[MAXC];
+  bool sec[MAXC];
+  float bvs[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int cb = wave + NW * c;
+    sec[c] = cb >= NCB1;
+    Pc[c] = sec[c] ? P2 : P1;
+    cbs[c] = sec[c] ? cb - NCB1 : cb;
+    const int col = cbs[c] * 16 + l15;
+    const float* bb = sec[c] ? b2 : b1;
+    const int nn = sec[c] ? N2 : N1;
+    bvs[c] = (bb && col < nn) ? gload(bb + col) : 0.f;
+  }
+  f32x4 acc[RB][MAXC];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int PFP = RING > 0 ? RING : PF_D;
+  f32x4 bq[PFP][MAXC];
+#pragma unroll
+  for (int u = 0; u < PFP - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) bq[u][c] = load_pk(Pc[c], cbs[c], u < NK ? u : NK - 1, NK);
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    if (s + PFP - 1 < NK) {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) bq[(s + PFP - 1) % PFP][c] = load_pk(Pc[c], cbs[c], s + PFP - 1, NK);
+    }
+    f32x4 a1[RB], a2[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      a1[rb] = *reinterpret_cast<const f32x4*>(in1 + (rb * 16 + l15) * ldi + 16 * s + 4 * g);
+      a2[rb] = *reinterpret_cast<const f32x4*>(in2 + (rb * 16 + l15) * ldi + 16 * s + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(sec[c] ? a2[rb][m] : a1[rb][m], bq[s % PFP][c][m],
+                                                            acc[rb][c], 0, 0, 0);
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int cb = wave + NW * c;
+    if (cb >= NCB1 + NCB2) continue;
+    float* out = sec[c] ? out2 : out1;
+    const int nn = sec[c] ? N2 : N1;
+    const GSave& gs = sec[c] ? gs2 : gs1;
+    const int col = cbs[c] * 16 + l15;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * 16 + 4 * g + r;
+        const float z = acc[rb][c][r] + bvs[c];
+        const float y = act_fn<ACT>(z);
+        if (out) out[row * ldo + col] = (col < nn) ? y : 0.f;
+        if (col < nn && row < gs.nrows) {
+          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+        }
+      }
+  }
+}
+
+template <int NW, int RB, int NC, int ACT, int NK, int RING>
+__device__ __forceinline__ void tile_dense_pair2_nc(int nc, const float* in1, const float* in2, int ldi,
+                                                    const float* P1, const float* b1, int N1, float* out1,
+                                                    const float* P2, const float* b2, int N2, float* out2, int ldo,
+                                                    const GSave& gs1, const GSave& gs2) {
+  if (nc == NC)
+    tile_dense_pair2_core<NW, RB, NC, ACT, NK, RING>(in1, in2, ldi, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1, gs2);
+  else if constexpr (NC > 1)
+    tile_dense_pair2_nc<NW, RB, NC - 1, ACT, NK, RING>(nc, in1, in2, ldi, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1,
+                                                       gs2);
+}
+
+template <int NW, int RB, int MAXC, int ACT, int NK, int RING = 0>
+__device__ __forceinline__ void tile_dense_pair2(const float* in1, const float* in2, int ldi, const float* P1,
+                                                 const float* b1, int N1, float* out1, const float* P2,
+                                                 const float* b2, int N2, float* out2, int ldo,
+                                                 const GSave& gs1 = GSave{nullptr, nullptr, 0, 0},
+                                                 const GSave& gs2 = GSave{nullptr, nullptr, 0, 0}) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NCB = ((N1 + 15) >> 4) + ((N2 + 15) >> 4);
+  const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
+  tile_dense_pair2_nc<NW, RB, MAXC, ACT, NK, RING>(nc, in1, in2, ldi, P1, b1, N1, out1, P2, b2, N2, out2, ldo, gs1, gs2);
+}
+
+// out = act([in1 | in2] x [P1; P2] + bias): one layer whose K is the concatenation of
+// two inputs (NK k-steps each) with their own packed mirrors -- the sum of two heads'
+// contributions to a shared trunk gradient as ONE product (one pipeline fill, one
+// epilogue, no intermediate LDS round trip).
+template <int NW, int RB, int MAXC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_catk_core(const float* in1, const float* in2, int ldi,
+                                                     const float* __restrict__ P1, const float* __restrict__ P2,
+                                                     const float* __restrict__ bias, int N, float* out, int ldo,
+                                                     const GSave& gs) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, g = lane >> 4;
+  int cbs[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) cbs[c] = wave + NW * c;
+  f32x4 acc[RB][MAXC];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int PF = pf_depth<MAXC>();
+  constexpr int NS = 2 * NK;
+  f32x4 bq[PF][MAXC];
+  // k-step s of the concatenation: s < NK from (in1, P1), else (in2, P2) at s - NK
+  auto frag = [&](int c, int s) { return s < NK ? load_pk(P1, cbs[c], s, NK) : load_pk(P2, cbs[c], s - NK, NK); };
+  auto afrag = [&](int rb, int s) {
+    const float* in = s < NK ? in1 : in2;
+    const int ks = s < NK ? s : s - NK;
+    return *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 16 * ks + 4 * g);
+  };
+#pragma unroll
+  for (int u = 0; u < PF - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) bq[u][c] = frag(c, u);
+  float bvs[MAXC];
+  load_bias<NW, MAXC>(bias, N, bvs);
+  f32x4 an[RB], ac[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) an[rb] = afrag(rb, 0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s + PF - 1 < NS) {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) bq[(s + PF - 1) % PF][c] = frag(c, s + PF - 1);
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
+    if (s + 1 < NS) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) an[rb] = afrag(rb, s + 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF][c][m], acc[rb][c], 0, 0, 0);
+  }
+  dense_epilogue<NW, RB, MAXC, ACT>(acc, bvs, N, out, ldo, gs);
+}
+
+template <int NW, int RB, int NC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_catk_nc(int nc, const float* in1, const float* in2, int ldi, const float* P1,
+                                                   const float* P2, const float* bias, int N, float* out, int ldo,
+                                                   const GSave& gs) {
+  if (nc == NC) tile_dense_catk_core<NW, RB, NC, ACT, NK>(in1, in2, ldi, P1, P2, bias, N, out, ldo, gs);
+  else if constexpr (NC > 1) tile_dense_catk_nc<NW, RB, NC - 1, ACT, NK>(nc, in1, in2, ldi, P1, P2, bias, N, out, ldo, gs);
+}
+
+template <int NW, int RB, int MAXC, int ACT, int NK>
+__device__ __forceinline__ void tile_dense_catk(const float* in1, const float* in2, int ldi, const float* P1,
+                                                const float* P2, const float* bias, int N, float* out, int ldo,
+                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NCB = (N + 15) >> 4;
+  const int nc = wave < NCB ? min(MAXC, (NCB - wave + NW - 1) / NW) : 0;
+  tile_dense_catk_nc<NW, RB, MAXC, ACT, NK>(nc, in1, in2, ldi, P1, P2, bias, N, out, ldo, gs);
+}
+
 // Partials-only form of tile_dense_narrow_pair (below): the value of layer `which`
 // at (row, col) is narrow_pair_sum<NW, RB>(red, which, row, col) + its bias, in the
 // same summation order as tile_dense_narrow_pair's epilogue.

@@ -510,6 +510,100 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__
   return cur;
 }
 
+// Two heads of the same shape on a shared trunk (the dynamics model's diff / log-var
+// heads, src/dynamics.py:84-91; the constraint critic's mean / log-std heads,
+// src/ssac.py:46-92), each [trunk width -> H -> out] with an identity output layer:
+// backed through TOGETHER. Their output layers' products run side by side (one
+// two-input pair layer), and the trunk-output gradient -- the sum of the two heads'
+// hidden-layer products -- is ONE product with the concatenated K (dZ_1 | dZ_2) x
+// [W_1; W_2]: three dependent GEMM phases instead of five, and no LDS accumulation.
+__device__ __forceinline__ bool bwd_paired_heads(const drpo_mlp_bwd_t& a) {
+  if (!a.trunk || a.split_heads || a.nnets != 3) return false;
+  const drpo_mlp_bwd_net_t &h1 = a.net[1], &h2 = a.net[2];
+  if (h1.nl != 2 || h2.nl != 2 || h1.dx || h2.dx) return false;
+  for (int l = 0; l < 2; ++l)
+    if (h1.L[l].din != h2.L[l].din || h1.L[l].dout != h2.L[l].dout || h1.L[l].act != h2.L[l].act) return false;
+  const int hid = h1.L[0].dout, out = h1.L[1].dout;
+  return h1.L[1].act == ACT_NONE && (hid == 200 || hid == 256) && out <= 64 && h1.L[0].din <= 256;
+}
+
+template <int NK>
+__device__ __forceinline__ void bwd_heads_catk(const drpo_mlp_bwd_net_t& h1, const drpo_mlp_bwd_net_t& h2, const float* D1,
+                                               const float* D2, float* out, int z) {
+  tile_dense_catk<FW_NW, 1, FW_MAXC, ACT_NONE, NK>(D1, D2, LDH, h1.L[0].W + (size_t)z * h1.L[0].wstride,
+                                                   h2.L[0].W + (size_t)z * h2.L[0].wstride, nullptr, h1.L[0].din, out,
+                                                   LDH);
+}
+
+template <int NK>
+__device__ __forceinline__ void bwd_heads_out(const drpo_mlp_bwd_net_t& h1, const drpo_mlp_bwd_net_t& h2, const float* G1,
+                                              const float* G2, float* o1, float* o2, int z) {
+  const int hid = h1.L[1].din;
+  tile_dense_pair2<FW_NW, 1, 4, ACT_NONE, NK, 2>(G1, G2, LDH, h1.L[1].W + (size_t)z * h1.L[1].wstride, nullptr, hid, o1,
+                                              h2.L[1].W + (size_t)z * h2.L[1].wstride, nullptr, hid, o2, LDH);
+}
+
+// heads' output gradients -> trunk-output gradient in G (bA, bB, DT are scratch)
+__device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restrict__ a, float* G, float* bA, float* bB,
+                                                 float* DT, int z, int row0, int nrows) {
+  const int tid = threadIdx.x;
+  const drpo_mlp_bwd_net_t &h1 = a.net[1], &h2 = a.net[2];
+  const int hid = h1.L[0].dout, out = h1.L[1].dout;
+  const int opad = round_up(out, 16), hpad = round_up(hid, 16);
+  float sv1[BW_PER], sv2[BW_PER];
+  bwd_fetch_act(h1.L[0], z, a.rows, row0, nrows, sv1);   // head 1's hidden saved values, one phase ahead
+  // output layers (identity): dZ = the given output gradient, saved for the weight gradients
+  const size_t so = ((size_t)z * a.rows + row0) * out;
+  for (int e = tid; e < 2 * FW_ROWS * opad; e += FW_NT) {
+    const int w = e / (FW_ROWS * opad), e2 = e - w * FW_ROWS * opad;
+    const int r = e2 / opad, k = e2 - r * opad;
+    const drpo_mlp_bwd_net_t& h = w ? h2 : h1;
+    float gv = 0.f;
+    if (r < nrows && k < out) {
+      gv = gload(h.gout + so + (size_t)r * out + k);
+      if (h.L[1].dz) gstore(h.L[1].dz + so + (size_t)r * out + k, gv);
+    }
+    (w ? bA : G)[r * LDH + k] = gv;
+  }
+  lds_barrier();
+  // dY(hidden) of both heads: one two-input pair layer (K = out)
+  switch ((out + 15) >> 4) {
+    case 1: bwd_heads_out<1>(h1, h2, G, bA, bB, DT, z); break;
+    case 2: bwd_heads_out<2>(h1, h2, G, bA, bB, DT, z); break;
+    case 3: bwd_heads_out<3>(h1, h2, G, bA, bB, DT, z); break;
+    default: bwd_heads_out<4>(h1, h2, G, bA, bB, DT, z); break;
+  }
+  bwd_fetch_act(h2.L[0], z, a.rows, row0, nrows, sv2);   // (after the product: 128-VGPR budget)
+  lds_barrier();
+  // hidden activations' gradient, saved dZ
+  const size_t sh = ((size_t)z * a.rows + row0) * hid;
+  const int act = h1.L[0].act;
+#pragma unroll
+  for (int i = 0; i < BW_PER; ++i) {
+    const int e = tid + i * FW_NT;
+    if (e >= FW_ROWS * hpad) break;
+    const int r = e / hpad, k = e - r * hpad;
+    float g1 = 0.f, g2 = 0.f;
+    if (r < nrows && k < hid) {
+      g1 = bB[r * LDH + k];
+      g2 = DT[r * LDH + k];
+      if (act != ACT_NONE) {
+        g1 *= act_grad_saved(act, sv1[i]);
+        g2 *= act_grad_saved(act, sv2[i]);
+      }
+      if (h1.L[0].dz) gstore(h1.L[0].dz + sh + (size_t)r * hid + k, g1);
+      if (h2.L[0].dz) gstore(h2.L[0].dz + sh + (size_t)r * hid + k, g2);
+    }
+    bB[r * LDH + k] = g1;
+    DT[r * LDH + k] = g2;
+  }
+  lds_barrier();
+  // trunk-output gradient = dZ_1 W_1 + dZ_2 W_2 as one concatenated-K product
+  if (hid == 200) bwd_heads_catk<13>(h1, h2, bB, DT, G, z);
+  else bwd_heads_catk<16>(h1, h2, bB, DT, G, z);
+  lds_barrier();
+}
+
 // one (job, net) slot of the fused backward-data pass; `a` may live in kernarg
 // (single launch) or global memory (multi-job launch)
 __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, int sel, int bx, int bz, float* smem) {
@@ -556,6 +650,12 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     load_gout(n, G);
     float* gh = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, true);
     bwd_net(a.net[0], gh, bA, bB, z, a.rows, row0, nrows, false, sel == 1);
+    return;
+  }
+  if (bwd_paired_heads(a)) {
+    bwd_heads_paired(a, G, bA, bB, DT, z, row0, nrows);
+    const float* gx = bwd_net(a.net[0], G, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
+    if (gx) store_dx(a.net[0], gx);
     return;
   }
   const int tw = a.net[0].L[a.net[0].nl - 1].dout;

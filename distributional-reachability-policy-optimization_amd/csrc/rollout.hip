@@ -686,16 +686,26 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         else rew[r] = x;
       }
     } else {
-      tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
-      lds_barrier();
-      if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm, red);
-      else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm);
-      lds_barrier();
-      tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, lW1, lb1, Hm, h1, ldh);
-      lds_barrier();
-      if (t == 2) RSTAMP(7);
-      if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm, red);
-      else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm);
+      if (Hm == 200 && 2 * ((S1 + 15) >> 4) <= NW) {
+        // wide state (tracking, S + 1 = 52): the two hidden layers as one 400-wide layer,
+        // then both output layers side by side (two inputs, one block per wave): two
+        // phases instead of four
+        tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
+        lds_barrier();
+        if (t == 2) RSTAMP(7);
+        tile_dense_pair2<NW, RB, 1, ACT_NONE, 13>(h1, h3, ldh, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm);
+      } else {
+        tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
+        lds_barrier();
+        if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm, red);
+        else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm);
+        lds_barrier();
+        tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, lW1, lb1, Hm, h1, ldh);
+        lds_barrier();
+        if (t == 2) RSTAMP(7);
+        if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm, red);
+        else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm);
+      }
       lds_barrier();
       // residual mean, log-var soft clamp, Gaussian sample
       for (int e = tid; e < ROWS * S1; e += NT) {
@@ -762,380 +772,6 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
 }
 
 #undef PERSIST_LDS_LAYOUT
-
-// ---------------------------------------------------------------------------
-// Fused-horizon engine, restructured step (rollout_persist2_kernel; reference widths:
-// actor hidden 256, model hidden 200). Against rollout_persist_kernel it takes three
-// latency-bound phases off each step's critical chain:
-//  * the member's first layer is split by input: its normalised-state part (K = S) is
-//    computed for step t+1 together with the actor's first layer of step t+1 (both
-//    depend only on s_{t+1}) in the phase that evaluates step t's constraints, staging
-//    and draws, on the waves the constraint wave leaves idle; the action part (K = A,
-//    a rank-A update) is applied elementwise with the SiLU once the action is sampled;
-//  * the actor's output head (256 -> 2A) is reduced straight from the hidden layer's
-//    accumulators (per-lane products + a 16-lane DPP row sum) instead of a separate
-//    split-K layer over an LDS copy of the hidden activations;
-//  * the action sample and the member-layer epilogue share one phase (each thread
-//    recomputes its row's action from the head partials).
-// Phases per step: A actor L2 (+ head partials) | B sample + member L1 epilogue |
-// C member L2 | D diff+log-var hidden (one 400-wide layer) | E output heads + Gaussian
-// sample | F constraints, staging, next draws, next L1s. Six barriers.
-// ---------------------------------------------------------------------------
-
-// sum over the 16 lanes of a DPP row (lanes 16g .. 16g+15); every lane gets the sum
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));    // quad [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));    // quad [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));   // row_half_mirror
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));   // row_mirror
-  return v;
-}
-
-// the K = S first layers of the NEXT step, from its states in xin: the actor's layer 1
-// (ReLU -> h1) and the member's normalised-state part (pre-activation + bias -> zm), as
-// 16-column jobs spread over waves [w0, NW); plus the member's action columns -> w1a.
-template <int NW, int RB, bool LW>
-__device__ __forceinline__ void persist2_first_layers(const PersistArgs& p, const float* xin, int ldx, float* h1,
-                                                      float* zm, int ldh, const float* v_nm, const float* v_ns,
-                                                      const float* wl1, float* w1a, int m, int w0) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l15 = lane & 15, g = lane >> 4;
-  const int S = p.S, A = p.A, Ha = p.Ha, Hm = p.Hm;
-  const int nks = (S + 15) >> 4;                 // k-steps of the K = S products
-  const int nks_m = (S + A + 15) >> 4;           // k-step stride of the member's packed mirror
-  const float* aW1 = step_opaque(p.aW1);
-  const float* ab1 = step_opaque(p.ab1);
-  const float* mW1 = p.mW1 + (size_t)m * p.ms_in;
-  const float* mb1 = p.mb1 + (size_t)m * Hm;
-  if (wave < w0) return;
-  // the member's action columns W1[c][S + d] (packed mirror) for the rank-A update
-  for (int e = tid - 64 * w0; e < Hm * A; e += (NW - w0) * 64) {
-    const int c = e / A, d = e - c * A, k = S + d;
-    w1a[d * 256 + c] = gload(mW1 + ((size_t)((c >> 4) * nks_m + (k >> 4)) << 8) + 4 * ((c & 15) + 16 * ((k & 15) >> 2)) +
-                             (k & 3));
-  }
-  const int nja = Ha >> 4, njm = (Hm + 15) >> 4;
-  for (int j = wave - w0; j < nja + njm; j += NW - w0) {
-    const bool member = j >= nja;
-    const int cb = member ? j - nja : j;
-    f32x4 acc[RB];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < nks; ++s) {
-      f32x4 b;
-      if (!member && LW)
-        b = *(const __attribute__((address_space(3))) f32x4*)(wl1 + (cb << 8) + (lane << 2));
-      else
-        b = member ? load_pk(mW1, cb, s, nks_m) : load_pk(aW1, cb, s, nks);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        f32x4 a = *reinterpret_cast<const f32x4*>(xin + (rb * 16 + l15) * ldx + 16 * s + 4 * g);
-        if (member) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int k = 16 * s + 4 * g + i;
-            a[i] = k < S ? (a[i] - v_nm[k]) / v_ns[k] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[i], acc[rb], 0, 0, 0);
-      }
-    }
-    const int col = cb * 16 + l15;
-    const float bv = member ? (col < Hm ? gload(mb1 + col) : 0.f) : gload(ab1 + col);
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + r;
-        const float z = acc[rb][r] + bv;
-        if (member) zm[row * ldh + col] = col < Hm ? z : 0.f;
-        else h1[row * ldh + col] = z > 0.f ? z : 0.f;
-      }
-  }
-}
-
-template <int RB, int NW, bool LW, int NA2>
-__global__ __launch_bounds__(NW * 64) void rollout_persist2_kernel(PersistArgs p) {
-  constexpr int ROWS = RB * 16;
-  constexpr int NT = NW * 64;
-  constexpr int MAXC = (16 + NW - 1) / NW;      // column blocks per wave for widths <= 256
-  constexpr int PMAXC = (32 + NW - 1) / NW;     // paired 200-wide layers: 26 blocks
-  constexpr int TPR = NT / ROWS;                // threads per row in the sample / epilogue phase
-  constexpr int A_ = NA2 / 2;
-  static_assert(NT % ROWS == 0, "rows must divide the workgroup");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x;
-  const int S = p.S, C = p.C, S1 = p.S + 1, B = p.B;
-  if (p.base_slot && blockIdx.x == 0 && tid == 0) *p.base_slot = *p.vptr_in;
-
-#define PERSIST2_LDS_LAYOUT(ZO, LDX, LDH, LDM, LDSS)                                          \
-  float* xin = smem + (ZO);                  /* ROWS x ldx  states (cols >= S stay 0) */       \
-  float* h1 = xin + ROWS * (LDX);                                                             \
-  float* h2 = h1 + ROWS * (LDH);                                                              \
-  float* h3 = h2 + ROWS * (LDH);             /* log-var hidden; member L1 state part (zm) */    \
-  float* sraw = h3 + ROWS * (LDH);           /* ROWS x lds  states at the start of the step */  \
-  float* ao = sraw + ROWS * (LDSS);                                                           \
-  float* dout = ao + ROWS * 20;                                                               \
-  float* lout = dout + ROWS * (LDM);                                                          \
-  float* act = lout + ROWS * (LDM);          /* ROWS x 8 */                                     \
-  float* rew = act + ROWS * 8;                                                                \
-  float* hval = rew + ROWS;                                                                   \
-  float* nz_a = hval + ROWS * 8;                                                              \
-  float* nz_m = nz_a + ROWS * 8;                                                              \
-  int* flags = reinterpret_cast<int*>(nz_m + ROWS * 64);                                      \
-  int* alive = flags + ROWS;                                                                  \
-  int* s_nalive = alive + ROWS;                                                               \
-  float* red = reinterpret_cast<float*>(s_nalive + 4);                                        \
-  float* vecs = red + NW * RB * 256;          /* 4 x 64 normalizer / log-var bounds, 64 head bias */ \
-  float* v_nm = vecs;                                                                         \
-  float* v_ns = vecs + 64;                                                                    \
-  float* v_lo = vecs + 128;                                                                   \
-  float* v_hi = vecs + 192;                                                                   \
-  float* v_b3 = vecs + 256;                                                                   \
-  float* w1a = vecs + 320;                   /* A x 256: the member's action columns */        \
-  float* wl1 = w1a + A_ * 256;               /* LW: actor L1 mirror [16 cb][256] */              \
-  float* wl3 = wl1 + 16 * 256;               /* LW: actor head mirror [16 k-steps][256] */       \
-  float* wl2 = wl3 + 16 * 256;               /* LW: actor L2 [16 cb][PERSIST_L2_LDS][256] */     \
-  (void)ao; (void)dout; (void)lout; (void)act; (void)rew; (void)hval; (void)nz_a; (void)nz_m;   \
-  (void)flags; (void)alive; (void)s_nalive; (void)red; (void)v_nm; (void)v_ns; (void)v_lo; (void)v_hi; \
-  (void)v_b3; (void)w1a; (void)wl1; (void)wl2; (void)wl3;
-  const int tile = blockIdx.x;
-  const int row0 = tile * ROWS;
-  const int nrows = min(ROWS, B - row0);
-  const int Hm = p.Hm;
-  {
-  PERSIST2_LDS_LAYOUT(0, p.ldx, p.ldh, p.ldm, p.lds)
-  if (tid < 256) {
-    const int j = tid & 63, w = tid >> 6;
-    if (w == 0 && j < S) v_nm[j] = p.norm_mean[j];
-    if (w == 1 && j < S) v_ns[j] = p.norm_std[j] + 1e-6f;
-    if (w == 2 && j < S1) v_lo[j] = p.min_lv[j];
-    if (w == 3 && j < S1) v_hi[j] = p.max_lv[j];
-  } else if (tid < 256 + NA2) {
-    v_b3[tid - 256] = p.ab3[tid - 256];
-  }
-  if constexpr (LW) {
-    const f32x4* a1 = reinterpret_cast<const f32x4*>(p.aW1);
-    const f32x4* a3 = reinterpret_cast<const f32x4*>(p.aW3);
-    const f32x4* a2 = reinterpret_cast<const f32x4*>(p.aW2);
-    for (int e = tid; e < 16 * 64; e += NT) {
-      reinterpret_cast<f32x4*>(wl1)[e] = gload(a1 + e);
-      reinterpret_cast<f32x4*>(wl3)[e] = gload(a3 + e);
-    }
-    for (int e = tid; e < 16 * PERSIST_L2_LDS * 64; e += NT) {
-      const int cb = e / (PERSIST_L2_LDS * 64), r = e - cb * PERSIST_L2_LDS * 64;
-      reinterpret_cast<f32x4*>(wl2)[e] = gload(a2 + cb * 16 * 64 + r);
-    }
-  }
-  const int kpad = round_up(S + p.A, 16);
-  for (int e = tid; e < ROWS * kpad; e += NT) {
-    const int r = e / kpad, k = e - r * kpad;
-    float v = 0.f;
-    if (r < nrows && k < S) {
-      const int64_t c = p.init_idx ? p.init_idx[row0 + r]
-                                   : prp_index((uint64_t)(row0 + r), (uint64_t)p.replay_len, p.prp_half_bits, p.prp_key);
-      const int64_t phys = (p.replay_ptr > p.replay_cap) ? (p.replay_ptr % p.replay_cap + c) % p.replay_cap : c;
-      v = p.replay_states[phys * S + k];
-    }
-    xin[r * p.ldx + k] = v;
-    if (k < S) sraw[r * p.lds + k] = v;
-  }
-  if (tid < ROWS) alive[tid] = tid < nrows;
-  persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, p.A, S1, B, 0, row0, nrows, nz_a, nz_m, 0, NT);
-  lds_barrier();
-  persist2_first_layers<NW, RB, LW>(p, xin, p.ldx, h1, h3, p.ldh, v_nm, v_ns, wl1, w1a, p.members[0], 0);
-  lds_barrier();
-  }
-  for (int t = 0; t < p.H; ++t) {
-    int zo = 0, ldx = p.ldx, ldh = p.ldh, ldm = p.ldm, ldss = p.lds;
-    asm volatile("" : "+s"(zo), "+s"(ldx), "+s"(ldh), "+s"(ldm), "+s"(ldss));
-    PERSIST2_LDS_LAYOUT(zo, ldx, ldh, ldm, ldss)
-    const int lane = tid & 63, wave = tid >> 6, l15 = lane & 15, g = lane >> 4;
-    const int m = p.members[t];
-    const float* mW2 = p.mW2 + (size_t)m * p.ms_hid;
-    const float* dW1 = p.dW1 + (size_t)m * p.ms_hid;
-    const float* dW2 = p.dW2 + (size_t)m * p.ms_out;
-    const float* lW1 = p.lW1 + (size_t)m * p.ms_hid;
-    const float* lW2 = p.lW2 + (size_t)m * p.ms_out;
-    const float* mb2 = p.mb2 + (size_t)m * Hm;
-    const float* db1 = p.db1 + (size_t)m * Hm;
-    const float* db2 = p.db2 + (size_t)m * S1;
-    const float* lb1 = p.lb1 + (size_t)m * Hm;
-    const float* lb2 = p.lb2 + (size_t)m * S1;
-    int* alive_cur = (t & 1) ? flags : alive;
-    int* alive_nxt = (t & 1) ? alive : flags;
-    if (t == 2) RSTAMP(0);
-
-    // ---- A. actor L2 (256 -> 256, ReLU) + the output head's per-wave partials -------
-    {
-      constexpr int MC = 16 / NW;       // column blocks per wave of the 256-wide layer
-      float w3[MC][NA2];
-      const float* aW3 = step_opaque(p.aW3);
-#pragma unroll
-      for (int c = 0; c < MC; ++c)
-#pragma unroll
-        for (int o = 0; o < NA2; ++o) {
-          // packed head mirror: W3[o][k] at k-step k >> 4, lane o + 16 * ((k & 15) >> 2), element k & 3
-          const int idx = ((wave + NW * c) << 8) + 4 * (o + 16 * (l15 >> 2)) + (l15 & 3);
-          w3[c][o] = LW ? wl3[idx] : gload(aW3 + idx);
-        }
-      f32x4 acc[RB][MC];
-      float bvs[MC];
-      tile_dense_mma<NW, RB, MC, 16, LW ? PERSIST_L2_LDS : 0>(h1, ldh, step_opaque(p.aW2), step_opaque(p.ab2), 256,
-                                                             acc, bvs, wl2);
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float y[MC];
-#pragma unroll
-          for (int c = 0; c < MC; ++c) {
-            const float z = acc[rb][c][r] + bvs[c];
-            y[c] = z > 0.f ? z : 0.f;
-          }
-#pragma unroll
-          for (int o = 0; o < NA2; ++o) {
-            float q = 0.f;
-#pragma unroll
-            for (int c = 0; c < MC; ++c) q = fmaf(y[c], w3[c][o], q);
-            q = row16_sum(q);
-            if (l15 == 0) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + o] = q;
-          }
-        }
-    }
-    lds_barrier();
-    if (t == 2) RSTAMP(1);
-
-    // ---- B. squashed-Gaussian action + the member's first layer (state part + action
-    //         part, SiLU); TPR threads per row, each recomputes its row's action ---------
-    {
-      const int r = tid / TPR, q = tid - r * TPR;
-      float a[A_];
-#pragma unroll
-      for (int d = 0; d < A_; ++d) {
-        const float mu = narrow_sum<NW, RB>(red, r, d) + v_b3[d];
-        const float raw = narrow_sum<NW, RB>(red, r, A_ + d) + v_b3[A_ + d];
-        const float ls = -6.f + 10.f * sigmoidf(raw);
-        a[d] = tanhf(nz_a[r * 8 + d] * expf(ls) + mu);
-        if (q == 0) act[r * 8 + d] = a[d];
-      }
-      const int hp = round_up(Hm, 16);
-      for (int c = q; c < hp; c += TPR) {
-        float y = 0.f;
-        if (c < Hm) {
-          float z = h3[r * ldh + c];
-#pragma unroll
-          for (int d = 0; d < A_; ++d) z = fmaf(a[d], w1a[d * 256 + c], z);
-          y = act_fn<ACT_SILU>(z);
-        }
-        h1[r * ldh + c] = y;
-      }
-    }
-    lds_barrier();
-    if (t == 2) RSTAMP(2);
-
-    // ---- C. member L2 (200 -> 200, SiLU) ------------------------------------------------
-    tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, mW2, mb2, Hm, h2, ldh);
-    lds_barrier();
-    if (t == 2) RSTAMP(3);
-    // ---- D. diff and log-var hidden layers as one 400-wide layer over h2 -----------------
-    tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
-    lds_barrier();
-    if (t == 2) RSTAMP(4);
-
-    // ---- E. output heads + residual mean, log-var soft clamp, Gaussian sample -----------
-    if (S1 <= 16) {
-      float bd = 0.f, bl = 0.f;
-      if (tid < ROWS * S1) {
-        const int j = tid % S1;
-        bd = gload(db2 + j);
-        bl = gload(lb2 + j);
-      }
-      tile_dense_narrow_pair_partials<NW, RB>(h1, h3, ldh, Hm, dW2, lW2, red);
-      if (tid < ROWS * S1) {
-        const int r = tid / S1, j = tid - r * S1;
-        const float mean = (narrow_pair_sum<NW, RB>(red, 0, r, j) + bd) + (j < S ? sraw[r * ldss + j] : 0.f);
-        float lv = narrow_pair_sum<NW, RB>(red, 1, r, j) + bl;
-        lv = v_hi[j] - softplusf(v_hi[j] - lv);
-        lv = v_lo[j] + softplusf(lv - v_lo[j]);
-        const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
-        if (j < S) xin[r * ldx + j] = x;
-        else rew[r] = x;
-      }
-    } else {
-      // wide state (tracking, S + 1 = 52): both output layers side by side, one block each
-      tile_dense_pair<NW, RB, 1, ACT_NONE, 13>(h1, ldh, Hm, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm);
-      lds_barrier();
-      for (int e = tid; e < ROWS * S1; e += NT) {
-        const int r = e / S1, j = e - r * S1;
-        const float mean = dout[r * ldm + j] + (j < S ? sraw[r * ldss + j] : 0.f);
-        float lv = lout[r * ldm + j];
-        lv = v_hi[j] - softplusf(v_hi[j] - lv);
-        lv = v_lo[j] + softplusf(lv - v_lo[j]);
-        const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
-        if (j < S) xin[r * ldx + j] = x;
-        else rew[r] = x;
-      }
-    }
-    lds_barrier();
-    if (t == 2) RSTAMP(5);
-
-    // ---- F. constraints + alive map + their staging (wave 0, one lane per row); states /
-    //         actions staging and the state hand-off (waves 1 .. NW/2-1); the next step's
-    //         draws (waves NW/2 ..); the next step's first layers (waves 1 ..) ------------
-    const size_t sb = (size_t)t * B + row0;
-    static_assert(ROWS <= 64, "one constraint lane per row");
-    if (wave == 0) {
-      bool in_r = false, dn = false, vl = false;
-      if (tid < ROWS && alive_cur[tid]) {
-        float hh[8];
-        env_constraints_row(p.env, xin + tid * ldx, dn, vl, hh);
-        for (int c = 0; c < C; ++c) p.st_h[(sb + tid) * C + c] = hh[c];
-        p.st_r[sb + tid] = rew[tid];
-        p.st_dv[sb + tid] = (uint8_t)((dn ? 1 : 0) | (vl ? 2 : 0));
-        in_r = true;
-      }
-      const uint64_t mk = __ballot(in_r);
-      if (in_r) p.inv[((size_t)t * p.ntiles + tile) * ROWS + __popcll(mk & ((1ull << tid) - 1ull))] = tid;
-      if (tid == 0) p.cnt[(size_t)t * p.ntiles + tile] = __popcll(mk);
-      const uint64_t still = __ballot(in_r && !dn);
-      if (tid < ROWS) alive_nxt[tid] = in_r && !dn;
-      if (tid == 0) *s_nalive = __popcll(still);
-    } else {
-      if (t + 1 < p.H)
-        persist2_first_layers<NW, RB, LW>(p, xin, ldx, h1, h3, ldh, v_nm, v_ns, wl1, w1a, p.members[t + 1], 1);
-      if (wave < NW / 2) {
-        constexpr int NS = NT / 2 - 64;
-        const int ts = tid - 64;
-        for (int e = ts; e < ROWS * S; e += NS) {
-          const int r = e / S, k = e - r * S;
-          const float x = xin[r * ldx + k];
-          if (alive_cur[r]) {
-            p.st_s[(sb + r) * S + k] = sraw[r * ldss + k];
-            p.st_s2[(sb + r) * S + k] = x;
-          }
-          sraw[r * ldss + k] = x;
-        }
-        for (int e = ts; e < nrows * A_; e += NS) {
-          const int r = e / A_, d = e - r * A_;
-          if (alive_cur[r]) p.st_a[(sb + r) * A_ + d] = act[r * 8 + d];
-        }
-      } else if (t + 1 < p.H) {
-        persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, A_, S1, B, t + 1, row0, nrows, nz_a, nz_m, NT / 2,
-                            NT / 2);
-      }
-    }
-    lds_barrier();
-    if (t == 2) RSTAMP(6);
-    const int n_alive = __builtin_amdgcn_readfirstlane(*s_nalive);
-    if (n_alive == 0) {
-      for (int t2 = t + 1 + tid; t2 < p.H; t2 += NT) p.cnt[(size_t)t2 * p.ntiles + tile] = 0;
-      break;
-    }
-  }
-#undef PERSIST2_LDS_LAYOUT
-}
 
 // per step t: exclusive prefix of the tile counts -> pos[t][tile], n[t]
 __global__ __launch_bounds__(256) void rollout_scan_kernel(const int* __restrict__ cnt, int* __restrict__ pos,
@@ -1402,12 +1038,6 @@ static size_t persist_lds_bytes(int S, int A, int Ha, int Hm, int rpt, int nw) {
                           (size_t)nw * (rpt / 16) * 256 + 256);
 }
 
-// LDS bytes of rollout_persist2_kernel: the v1 layout + 64 head-bias floats + the
-// member's A action columns (A x 256)
-static size_t persist2_lds_bytes(int S, int A, int Ha, int Hm, int rpt, int nw) {
-  return persist_lds_bytes(S, A, Ha, Hm, rpt, nw) + sizeof(float) * (size_t)(64 + 256 * A);
-}
-
 // engine 2: fused-horizon kernel + count scan + ordered emit + pointer advance
 static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hipStream_t stream) {
   DRPO_REQUIRE(d->H <= PERSIST_MAX_H, "drpo_rollout: engine 2 supports horizon <= %d", PERSIST_MAX_H);
@@ -1450,10 +1080,7 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
     return (e && atoi(e) == 16) ? 16 : 8;
   }();
   const int nw = rpt == 32 ? 8 : NW;
-  // restructured step (rollout_persist2_kernel) at the reference widths
-  static const bool v1_only = getenv("DRPO_ROLLOUT_V1") != nullptr;   // A/B: the previous step structure
-  const bool v2 = !v1_only && d->Ha == 256 && d->Hm == 200 && (A == 1 || A == 2);
-  const size_t lds_bytes = v2 ? persist2_lds_bytes(S, A, d->Ha, d->Hm, rpt, nw) : persist_lds_bytes(S, A, d->Ha, d->Hm, rpt, nw);
+  const size_t lds_bytes = persist_lds_bytes(S, A, d->Ha, d->Hm, rpt, nw);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
   // LDS-resident actor weights (see rollout_persist_kernel) when they fit
   const size_t lw_bytes = sizeof(float) * (size_t)(32 + 16 * PERSIST_L2_LDS) * 256;
@@ -1466,23 +1093,7 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
     a.base_slot = off + H + 1;
   }
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
-  if (v2) {
-#define PERSIST2_LAUNCH(NA2)                                                                            \
-    if (rpt == 32)                                                                                    \
-      rollout_persist2_kernel<2, 8, false, NA2><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);          \
-    else if (NW == 16)                                                                                \
-      rollout_persist2_kernel<1, 16, false, NA2><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);        \
-    else if (lw)                                                                                      \
-      rollout_persist2_kernel<1, 8, true, NA2><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a); \
-    else                                                                                              \
-      rollout_persist2_kernel<1, 8, false, NA2><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
-    if (A == 1) {
-      PERSIST2_LAUNCH(2)
-    } else {
-      PERSIST2_LAUNCH(4)
-    }
-#undef PERSIST2_LAUNCH
-  } else if (rpt == 32)
+  if (rpt == 32)
     rollout_persist_kernel<2, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   else if (NW == 16)
     rollout_persist_kernel<1, 16, false><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);
@@ -1547,7 +1158,7 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
   // 32-row tiles halve the weight bytes per MFMA once the batch fills the chip with
   // them (B >= 8192), when the wider tile still fits the LDS (not for tracking's S=51)
   const int rpt = d->rows_per_tile ? d->rows_per_tile
-                                   : (d->B >= 256 * 32 && persist2_lds_bytes(d->S, d->A, d->Ha, d->Hm, 32, 8) <= 160 * 1024
+                                   : (d->B >= 256 * 32 && persist_lds_bytes(d->S, d->A, d->Ha, d->Hm, 32, 8) <= 160 * 1024
                                           ? 32 : 16);
   DRPO_REQUIRE(rpt == 16 || rpt == 32, "drpo_rollout: rows_per_tile must be 16 or 32");
   const int S = d->S, A = d->A, S1 = d->S + 1;

@@ -96,8 +96,12 @@ def fused_stamps():
     L.drpo_debug_stamps_rollout.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device('cuda')
     hm = int(os.environ.get('DRPO_STAMPS_HM', '200'))   # model width (200 = reference; else the unpaired path)
-    alg = bench.make_alg(dev, 4096, 10, 7, 0, bench.QUAD_JSON, extra={'model_cfg': {'hidden_dim': hm}})
-    rep = bench.synth_replay('quadrotor', 100000, np.random.RandomState(0))
+    c = int(os.environ.get('DRPO_STAMPS_CONFIG', '2'))   # BASELINE config (bench.CONFIGS)
+    cd = bench.CONFIGS[c]
+    env = cd['env']
+    alg = bench.make_alg(dev, cd['B'], min(cd['H'], 10), cd['E'], 0, bench.ENV_JSON[env],
+                         extra={'model_cfg': {'hidden_dim': hm}}, env=env)
+    rep = bench.synth_replay(env, 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     bench.steady_mode(alg)
@@ -114,10 +118,10 @@ def fused_stamps():
              'pair L2+gauss', 'constr+staging']
     if hm != 200:
         names[7:9] = ['diff L1+L2, lv L1', 'lv L2, gauss']
-    if hm == 200 and not os.environ.get('DRPO_ROLLOUT_V1'):     # rollout_persist2_kernel phases
-        names = ['start', 'actor L2+head', 'sample+member L1', 'member L2', 'pair L1', 'pair L2+gauss',
-                 'constr+staging+next L1']
-    print('== rollout_persist_kernel step t=2 (B=4096, quadrotor): cycles per phase, mean over 256 workgroups')
+    elif env == 'tracking':
+        names[7:9] = ['pair L1', 'pair L2 (2 inputs) + gauss']
+    print(f'== rollout_persist_kernel step t=2 (config {c}: {env} B={cd["B"]} E={cd["E"]}): cycles per phase, '
+          'mean over the first 256 workgroups')
     tot = 0
     for c in range(1, len(names)):
         d = st[:, c] - st[:, c - 1]
