@@ -98,6 +98,21 @@ __device__ __forceinline__ float act_fn(float x) {
 
 // torch softplus(beta=1, threshold=20)
 __device__ __forceinline__ float softplusf(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+// Hardware-transcendental forms (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp each) for the
+// fused rollout's per-row epilogues, where the libm forms (range reduction, IEEE
+// division) cost more than the layer they follow (tracking: 4.4k cycles of 10.6k in the
+// output-head phase). Relative error ~1e-6 at the magnitudes on the path, inside the
+// rollout parity tolerance (2e-4).
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(1.44269504088896341f * x); }
+__device__ __forceinline__ float fast_softplus(float x) {   // max(x, 0) + log1p(exp(-|x|)), threshold 20
+  if (x > 20.f) return x;
+  const float y = __builtin_amdgcn_exp2f(-1.44269504088896341f * fabsf(x));
+  return fmaxf(x, 0.f) + 0.69314718055994531f * __builtin_amdgcn_logf(1.f + y);
+}
+__device__ __forceinline__ float fast_tanh(float x) {        // 1 - 2 / (exp(2x) + 1), saturating
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(2.88539008177792682f * x) + 1.f);
+}
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
 
 // ---------------------------------------------------------------------------
@@ -493,12 +508,14 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
 }
 
 // K (input width) -> compile-time k-step count for the widths on the path
-// (14/13/12/11 inputs -> 1 step, 200 -> 13, 256 -> 16), else the runtime loop.
+// (<= 16 inputs -> 1 step, 49..64 -> 4, 200 -> 13, 256 -> 16), else the runtime loop.
 template <int NW, int RB, int MAXC, int ACT>
 __device__ __forceinline__ void tile_dense(const float* in, int ldi, int K, const float* P, const float* bias, int N,
                                            float* out, int ldo, const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
   switch ((K + 15) >> 4) {
     case 1: tile_dense_impl<NW, RB, MAXC, ACT, 1>(in, ldi, K, P, bias, N, out, ldo, gs); break;
+    // tracking's 51 / 53 inputs: unrolled, so all four k-steps' fragments are in flight at once
+    case 4: tile_dense_impl<NW, RB, MAXC, ACT, 4>(in, ldi, K, P, bias, N, out, ldo, gs); break;
     case 13: tile_dense_impl<NW, RB, MAXC, ACT, 13>(in, ldi, K, P, bias, N, out, ldo, gs); break;
     case 16: tile_dense_impl<NW, RB, MAXC, ACT, 16>(in, ldi, K, P, bias, N, out, ldo, gs); break;
     default: tile_dense_impl<NW, RB, MAXC, ACT, 0>(in, ldi, K, P, bias, N, out, ldo, gs); break;
@@ -782,11 +799,14 @@ __device__ __forceinline__ void tile_dense_pair2_core(const float* in1, const fl
     const int nn = sec[c] ? N2 : N1;
     bvs[c] = (bb && col < nn) ? gload(bb + col) : 0.f;
   }
-  f32x4 acc[RB][MAXC];
+  // one block per wave: even / odd k-steps into two accumulators, two independent MFMA
+  // chains instead of one 4*NK-long dependent chain (summed in the epilogue)
+  constexpr int NACC = MAXC == 1 && NK > 1 ? 2 : 1;
+  f32x4 acc[RB][MAXC], acc2[RB][MAXC];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = acc2[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int PFP = RING > 0 ? RING : PF_D;
   f32x4 bq[PFP][MAXC];
 #pragma unroll
@@ -811,9 +831,16 @@ __device__ __forceinline__ void tile_dense_pair2_core(const float* in1, const fl
 #pragma unroll
       for (int c = 0; c < MAXC; ++c)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(sec[c] ? a2[rb][m] : a1[rb][m], bq[s % PFP][c][m],
-                                                            acc[rb][c], 0, 0, 0);
+        for (int rb = 0; rb < RB; ++rb) {
+          f32x4& ac = (NACC == 2 && (s & 1)) ? acc2[rb][c] : acc[rb][c];
+          ac = __builtin_amdgcn_mfma_f32_16x16x4f32(sec[c] ? a2[rb][m] : a1[rb][m], bq[s % PFP][c][m], ac, 0, 0, 0);
+        }
+  }
+  if constexpr (NACC == 2) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) acc[rb][c] += acc2[rb][c];
   }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {

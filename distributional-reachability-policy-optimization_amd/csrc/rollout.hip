@@ -642,8 +642,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         const int r = tid / A, d = tid - r * A;
         const float mu = narrow_sum<NW, RB>(red, r, d) + bmu;
         const float raw = narrow_sum<NW, RB>(red, r, A + d) + braw;
-        const float ls = -6.f + 10.f * sigmoidf(raw);
-        const float a = tanhf(nz_a[r * 8 + d] * expf(ls) + mu);
+        const float ls = -6.f + 10.f * fast_sigmoid(raw);
+        const float a = fast_tanh(nz_a[r * 8 + d] * fast_exp(ls) + mu);
         act[r * 8 + d] = a;
         xin[r * ldx + S + d] = a;
       }
@@ -679,9 +679,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         const int r = tid / S1, j = tid - r * S1;
         const float mean = (narrow_pair_sum<NW, RB>(red, 0, r, j) + bd) + (j < S ? sraw[r * ldss + j] : 0.f);
         float lv = narrow_pair_sum<NW, RB>(red, 1, r, j) + bl;
-        lv = v_hi[j] - softplusf(v_hi[j] - lv);
-        lv = v_lo[j] + softplusf(lv - v_lo[j]);
-        const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
+        lv = v_hi[j] - fast_softplus(v_hi[j] - lv);
+        lv = v_lo[j] + fast_softplus(lv - v_lo[j]);
+        const float x = mean + fast_exp(0.5f * lv) * nz_m[r * 64 + j];
         if (j < S) xin[r * ldx + j] = x;
         else rew[r] = x;
       }
@@ -693,7 +693,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
         lds_barrier();
         if (t == 2) RSTAMP(7);
-        tile_dense_pair2<NW, RB, 1, ACT_NONE, 13>(h1, h3, ldh, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm);
+        // one block per wave: a ring as deep as K (every fragment in flight at once), else
+        // this latency-bound layer waits one L2 round trip per few k-steps
+        tile_dense_pair2<NW, RB, 1, ACT_NONE, 13, 13>(h1, h3, ldh, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm);
       } else {
         tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
         lds_barrier();
@@ -707,14 +709,15 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         else tile_dense<NW, RB, MAXC, ACT_NONE>(h1, ldh, Hm, lW2, lb2, S1, lout, ldm);
       }
       lds_barrier();
+      if (t == 2) RSTAMP(10);
       // residual mean, log-var soft clamp, Gaussian sample
       for (int e = tid; e < ROWS * S1; e += NT) {
         const int r = e / S1, j = e - r * S1;
         const float mean = dout[r * ldm + j] + (j < S ? sraw[r * ldss + j] : 0.f);
         float lv = lout[r * ldm + j];
-        lv = v_hi[j] - softplusf(v_hi[j] - lv);
-        lv = v_lo[j] + softplusf(lv - v_lo[j]);
-        const float x = mean + sqrtf(expf(lv)) * nz_m[r * 64 + j];
+        lv = v_hi[j] - fast_softplus(v_hi[j] - lv);
+        lv = v_lo[j] + fast_softplus(lv - v_lo[j]);
+        const float x = mean + fast_exp(0.5f * lv) * nz_m[r * 64 + j];
         if (j < S) xin[r * ldx + j] = x;
         else rew[r] = x;
       }

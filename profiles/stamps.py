@@ -128,6 +128,9 @@ def fused_stamps():
         tot += d.mean()
         print(f'   {names[c]:12s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f}')
     print(f'   total {tot:.0f} cycles')
+    if env == 'tracking' and (st[:, 10] > 0).all():
+        d = st[:, 10] - st[:, 7]
+        print(f'   (of pair L2 + gauss: output layers {d.mean():.0f}, gauss {(st[:, 8] - st[:, 10]).mean():.0f})')
 
 
 if __name__ == '__main__' and os.environ.get('DRPO_STAMPS_ROLLOUT') == 'fused':
