@@ -7,7 +7,7 @@ shift || true
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-if [ $# -eq 0 ]; then set -- 2 3 4 5; fi
+if [ $# -eq 0 ]; then set -- 1 2 3 4 5; fi
 for c in "$@"; do
   EXTRA="--no-cpu-baseline"
   if [ "$c" = "2" ]; then EXTRA=""; fi
