@@ -48,7 +48,8 @@ class OptimSeg(ctypes.Structure):
                 ('lr_over_bc1', c_float), ('bc2_sqrt', c_float), ('beta1', c_float), ('beta2', c_float),
                 ('eps', c_float), ('weight_decay', c_float), ('zero_grad', c_int),
                 ('ema_target', P), ('ema_rate', c_float), ('ema_keep', c_float), ('map', P),
-                ('grad_from_sum', P), ('grad_sum_rows', c_int64), ('grad_scale', c_float)]
+                ('grad_from_sum', P), ('grad_sum_rows', c_int64), ('grad_from_sum_kind', c_int),
+                ('grad_scale', c_float)]
 
 
 class EnsReduce(ctypes.Structure):
@@ -185,7 +186,7 @@ PROTOTYPES.update({
     'drpo_cc_head': (c_int, [P, P, c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P]),
     'drpo_critic_head': (c_int, [POINTER(CriticHead), P]),
     'drpo_actor_upstream': (c_int, [c_int64, c_int, c_int, c_float, c_float, c_float, P, P, P, P, P, P, P, P, P, P,
-                                    c_float, P]),
+                                    c_float, c_float, c_float, c_float, P]),
     'drpo_squash_backward': (c_int, [c_int64, c_int, P, P, P, P, P, P, c_float, P, c_float, P, P, P]),
     'drpo_alpha_grad': (c_int, [P, P, c_int64, P, P]),
     'drpo_multiplier_head': (c_int, [c_int64, P, P, P, c_float, c_float, c_float, c_float, c_float, P, P, P]),

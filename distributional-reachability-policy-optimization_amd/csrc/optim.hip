@@ -357,10 +357,13 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
   const float coef = S.partial ? s_coef : 1.f;
   if (!live) return;
-  if (S.grad_from_sum) {   // SAC temperature: -exp(log_alpha) * alpha-loss sum / rows
+  if (S.grad_from_sum) {   // a scalar's gradient from a device loss sum (see drpo_optim_seg_t)
     const float gs = *S.grad_from_sum * (1.f / (float)S.grad_sum_rows);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) g[e] = -expf(p[e]) * gs;
+    for (int e = 0; e < 4; ++e) {
+      const float c = S.grad_from_sum_kind == 1 ? 1.f / (1.f + expf(-p[e])) : (S.grad_from_sum_kind == 2 ? 1.f : expf(p[e]));
+      g[e] = -c * gs;
+    }
   } else if (gscale != 1.f) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) g[e] *= gscale;

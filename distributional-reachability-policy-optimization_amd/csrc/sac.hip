@@ -296,16 +296,16 @@ DRPO_API int drpo_critic_head(const drpo_critic_head_t* p, drpo_stream_t stream_
 __global__ void actor_upstream_kernel(int64_t B, int C, int dist, float ratio, float lmin, float lmax,
                                       const float* lams, const float* mu_a, const float* ls_a, const float* mu_s,
                                       const float* ls_s, float* gq, float* gmu_a, float* gls_a, float* gmu_s,
-                                      float* gls_s, float ub) {
+                                      float* gls_s, float ub, float fixed_lam, float clb, float cub) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const float invB = 1.f / (float)B;
   // pass 1, loads only: the arg-max constraint of each side and its raw log-std (both
   // sides' loads are in flight together; no store sits between them)
   int bis[2] = {0, 0};
-  float lsb[2] = {0.f, 0.f};
-  float lam = gmu_a ? lams[i] : 0.f;
-  if (ub > 0.f) lam = ub / 2.f * (1.f + tanhf(lam / ub * 2.f));   // MLPMultiplier.forward transform
+  float lsb[2] = {0.f, 0.f}, best_a = 0.f;
+  float lam = gmu_a ? (lams ? lams[i] : fixed_lam) : 0.f;
+  if (lams && ub > 0.f) lam = ub / 2.f * (1.f + tanhf(lam / ub * 2.f));   // MLPMultiplier.forward transform
 #pragma unroll
   for (int side = 0; side < 2; ++side) {
     const float* mu = side ? mu_s : mu_a;
@@ -321,7 +321,10 @@ __global__ void actor_upstream_kernel(int64_t B, int C, int dist, float ratio, f
     }
     bis[side] = bi;
     lsb[side] = lbest;
+    if (!side) best_a = best;
   }
+  // scalar multiplier: the certificate term is clamp(Qc, lb, ub) -- no gradient outside
+  if (!lams && (best_a < clb || best_a > cub)) lam = 0.f;
   // pass 2, stores
   if (gq) gq[i] = -invB;
 #pragma unroll
@@ -347,12 +350,13 @@ __global__ void actor_upstream_kernel(int64_t B, int C, int dist, float ratio, f
 DRPO_API int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, float log_std_min,
                                  float log_std_max, const float* lams, const float* mu_a, const float* ls_a,
                                  const float* mu_s, const float* ls_s, float* gq, float* gmu_a, float* gls_a,
-                                 float* gmu_s, float* gls_s, float lam_upper_bound, drpo_stream_t stream_) {
+                                 float* gmu_s, float* gls_s, float lam_upper_bound, float fixed_lam,
+                                 float clamp_lb, float clamp_ub, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (B == 0) return DRPO_OK;
   actor_upstream_kernel<<<(unsigned)((B + 63) / 64), 64, 0, stream>>>(
       B, C, distributional, std_ratio, log_std_min, log_std_max, lams, mu_a, ls_a, mu_s, ls_s, gq, gmu_a, gls_a,
-      gmu_s, gls_s, lam_upper_bound);
+      gmu_s, gls_s, lam_upper_bound, fixed_lam, clamp_lb, clamp_ub);
   DRPO_LAUNCH_CHECK("actor_upstream");
   return DRPO_OK;
 }
@@ -444,7 +448,10 @@ __global__ __launch_bounds__(256) void multiplier_head_kernel(int64_t B, const f
   __shared__ float red[8];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float l = 0.f;
-  if (i < B) {
+  if (i < B && !x) {
+    // scalar multiplier: the penalty sum of -mean(softplus(m) * penalty)
+    l = fminf(fmaxf(aqc[i] - thr, plb), pub);
+  } else if (i < B) {
     const float t = tanhf(x[i] / ub * 2.f);
     const float lam = ub / 2.f * (1.f + t);
     const float pen = fminf(fmaxf(aqc[i] - thr, plb), pub);

@@ -101,9 +101,9 @@ def sync_parameters(alg, src=0):
     red = GradReducer()
     sol, m = alg.solver, alg.model_ensemble
     red.broadcast_(sol.actor.group.data, sol.actor_safe.group.data, sol.critic_group.data,
-                   sol.critic_target_group.data, sol.multiplier.group.data, sol.log_alpha, m.group.data,
+                   sol.critic_target_group.data, sol.multiplier_group.data, sol.log_alpha, m.group.data,
                    m.state_normalizer.mean, m.state_normalizer.std, src=src)
-    for g in (sol.actor.group, sol.actor_safe.group, sol.critic_group, sol.critic_target_group, sol.multiplier.group,
+    for g in (sol.actor.group, sol.actor_safe.group, sol.critic_group, sol.critic_target_group, sol.multiplier_group,
               m.group):
         g.mark_dirty()
 

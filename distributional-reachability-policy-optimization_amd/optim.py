@@ -67,11 +67,13 @@ class Adam:
             self.group.mark_dirty()
 
     def segment(self, start, end, scalars, clip=None, zero_grad=False, ema=None, pack_map=None, grad=None,
-                grad_from_sum=None, grad_scale=1.0):
+                grad_from_sum=None, grad_from_sum_kind=0, grad_scale=1.0):
         """drpo_optim_seg_t for elements [start, end) of this optimizer's tensor:
         clip = (partials, max_norm); ema = (target flat tensor, rate); pack_map = device
         drpo_pack_map_t of the group (refreshes its packed mirrors); grad_from_sum =
-        (device scalar sum, rows): gradient -exp(p) * sum / rows (the SAC temperature);
+        (device scalar sum, rows): gradient -c(p) * sum / rows of a scalar parameter, with
+        c = exp(p) (kind 0: the SAC temperature), sigmoid(p) (kind 1: the scalar
+        multiplier's softplus) or 1 (kind 2: the log-alpha loss);
         grad_scale: multiplier of the gradient (and of its clip norm) -- 1/G after a
         data-parallel SUM all-reduce, so the mean needs no separate pass."""
         from ._abi import OptimSeg
@@ -92,6 +94,7 @@ class Adam:
         sg.map = 0 if pack_map is None else pack_map.data_ptr()
         if grad_from_sum is not None:
             sg.grad_from_sum, sg.grad_sum_rows = grad_from_sum[0].data_ptr(), int(grad_from_sum[1])
+            sg.grad_from_sum_kind = int(grad_from_sum_kind)
         sg.grad_scale = float(grad_scale)
         return sg
 

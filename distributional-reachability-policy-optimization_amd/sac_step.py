@@ -240,7 +240,7 @@ class SACEngine:
         self.ws = {}
         sol, S, A, C = self.sol, self.S, self.A, self.C
         cg, tg = sol.critic_group, sol.critic_target_group
-        ag, sg, mg = sol.actor.group, sol.actor_safe.group, sol.multiplier.group
+        ag, sg, mg = sol.actor.group, sol.actor_safe.group, sol.multiplier_group
         cspec, ccs = sol.critic.spec, sol.constraint_critic
         buf = self.buf
 
@@ -264,7 +264,8 @@ class SACEngine:
             n['cc_trunk' + tag] = mk(grp, 'constraint_critic.trunk.', ccs.trunk_spec, gr)
             n['cc_mean' + tag] = mk(grp, 'constraint_critic.mean_head.', ccs.mean_spec, gr)
             n['cc_ls' + tag] = mk(grp, 'constraint_critic.log_std_head.', ccs.logstd_spec, gr)
-        n['mult'] = mk(mg, 'lam.', sol.multiplier.spec)
+        if sol.mlp_multiplier:
+            n['mult'] = mk(mg, 'lam.', sol.multiplier.spec)
         self.nets_view = {}
         # forward saves (post-activations) and dz for every trained net
         for key, net in n.items():
@@ -301,7 +302,7 @@ class SACEngine:
         """Refresh the packed weight mirrors of every group an update step reads."""
         sol = self.sol
         for g in (sol.actor.group, sol.actor_safe.group, sol.critic_group, sol.critic_target_group,
-                  sol.multiplier.group):
+                  sol.multiplier_group):
             g.ensure_packed()
 
     def _run_fwd(self, key, builder):
@@ -541,11 +542,13 @@ class SACEngine:
         ws = self.ws
         dist = sol.distributional_qc
         qshape = (B,) if C == 1 else (B, C)
+        mlp_mult = sol.mlp_multiplier
         e5 = self._eps('e5', noise.std_normal((B, A)))
         k = noise.choice(2)
         if dist:
-            noise.randn_like(qshape, used=False)
-            noise.randn_like(qshape, used=False)
+            noise.randn_like(qshape, used=False)       # Qc(s, a)
+            if mlp_mult:
+                noise.randn_like(qshape, used=False)   # Qc(s, tanh(mu_safe)) for lambda
         e6 = self._eps('e6', noise.std_normal((B, A)))
         if dist:
             noise.randn_like(qshape, used=False)
@@ -564,28 +567,33 @@ class SACEngine:
                       e6, SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am)], ctr)
         # launch 2: Q_k(s, a), Qc(s, a), Qc(s, a_safe) with saves; Qc(s, tanh(mu_safe)) for lam
         qk = n['q0'] if k == 0 else n['q1']
-        self._run_multi(f'a.f2.{k}', lambda: [
+        self._run_multi(f'a.f2.{k}{int(mlp_mult)}', lambda: [
             fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
             fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True),
-            fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True),
-            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)], ctr)
-        # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad)
-        sqc = self.buf('a.sqc', B)
-        self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
-        self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
-                                                 [(self.bs, S), (sqc, 1), (None, 0)], B))
+            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)] + ([
+            fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True)] if mlp_mult else []),
+            ctr)
+        if mlp_mult:
+            # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad)
+            sqc = self.buf('a.sqc', B)
+            self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
+            self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
+                                                     [(self.bs, S), (sqc, 1), (None, 0)], B))
         # upstream gradients; lam = MLPMultiplier's output transform of 'a.multx', applied
-        # inside actor_upstream (no separate multiplier_out launch)
+        # inside actor_upstream (no separate multiplier_out launch) -- or, with the scalar
+        # multiplier, lam = fixed_multiplier on clamp(Qc, penalty_lb, penalty_ub)
+        # (src/ssac.py:480-484)
         ca, cs = self._cc_views('a.cc'), self._cc_views('a.cc2')
         gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
                                     self.buf('a.gmu2', B, C), self.buf('a.gls2', B, C))
         ub = float(sol.mlp_multiplier_cfg.upper_bound)
-        assert ub > 0, 'MLPMultiplier upper_bound must be positive'
+        assert ub > 0 or not mlp_mult, 'MLPMultiplier upper_bound must be positive'
         _lib.check(L.drpo_actor_upstream(B, C, int(dist), float(cc.std_ratio), float(cc.log_std_min),
-                                         float(cc.log_std_max), ws['a.multx'].data_ptr(), ca[0].data_ptr(),
-                                         ca[1].data_ptr(), cs[0].data_ptr(), cs[1].data_ptr(), gq.data_ptr(),
-                                         gmu.data_ptr(), gls.data_ptr(), gmu2.data_ptr(), gls2.data_ptr(), ub,
-                                         _lib.stream()),
+                                         float(cc.log_std_max), ws['a.multx'].data_ptr() if mlp_mult else None,
+                                         ca[0].data_ptr(), ca[1].data_ptr(), cs[0].data_ptr(), cs[1].data_ptr(),
+                                         gq.data_ptr(), gmu.data_ptr(), gls.data_ptr(), gmu2.data_ptr(),
+                                         gls2.data_ptr(), ub, float(sol.fixed_multiplier), float(sol.penalty_lb),
+                                         float(sol.penalty_ub), _lib.stream()),
                    'actor_upstream')
         # dL/da of the actor (Q_k part + certificate part, summed in squash_backward in
         # the reference's order) and of the safe actor: one backward launch
@@ -631,16 +639,22 @@ class SACEngine:
         if aopt.tensor is None:
             aopt.tensor = sol.log_alpha.view(1)
         segs = [sol.actor_optimizer.segment(0, ga.size, sol.actor_optimizer.step_scalars(), clip=(pa, sol.grad_norm),
-                                            zero_grad=True, pack_map=ga.pack_map(), grad_scale=gsc),
-                aopt.segment(0, 1, aopt.step_scalars(), grad=ag, grad_from_sum=(asum, B * self.dp.world)),
-                sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
-                                                 clip=(ps, sol.grad_norm), zero_grad=True, pack_map=gs.pack_map(),
-                                                 grad_scale=gsc)]
+                                            zero_grad=True, pack_map=ga.pack_map(), grad_scale=gsc)]
+        # without autotune_alpha the reference's optimizer list is [actor, actor_safe], so
+        # its "i == 2" clip / schedule of the safe actor never fires (src/ssac.py:507-527)
+        safe_full = sol.autotune_alpha
+        if sol.autotune_alpha:
+            segs.append(aopt.segment(0, 1, aopt.step_scalars(), grad=ag, grad_from_sum=(asum, B * self.dp.world),
+                                     grad_from_sum_kind=2 if sol.use_log_alpha_loss else 0))
+        segs.append(sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
+                                                     clip=(ps, sol.grad_norm) if safe_full else None, zero_grad=True,
+                                                     pack_map=gs.pack_map(), grad_scale=gsc))
         fused_step(segs)
         self._grads_zeroed(ga)
         self._grads_zeroed(gs)
         sol.actor_lr_scheduler.step()
-        sol.actor_safe_lr_scheduler.step()
+        if safe_full:
+            sol.actor_safe_lr_scheduler.step()
 
     def _alpha_adam(self, grad):
         opt = self.sol.alpha_optimizer
@@ -688,6 +702,8 @@ class SACEngine:
         sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
         self._ensure_packed()
         self.noise = noise = noise or self.noise
+        if not sol.mlp_multiplier:
+            return self._scalar_mult_step(noise)
         L = _lib.lib()
         ws = self.ws
         dist = sol.distributional_qc
@@ -719,7 +735,7 @@ class SACEngine:
                                           float(sol.constraint_threshold), float(sol.penalty_lb),
                                           float(sol.penalty_ub), float(mc.upper_bound), float(sol.lam_epsilon),
                                           gx.data_ptr(), None, _lib.stream()), 'multiplier_head')
-        g = sol.multiplier.group
+        g = sol.multiplier_group
         self._clean_grads(g)
         nm = n['mult']
         self._run_bwd('m.bmult', lambda: fill_bwd([nm], [gx], B))
@@ -732,6 +748,38 @@ class SACEngine:
                                                      pack_map=g.pack_map(), grad_scale=self.dp.scale)])
         self._grads_zeroed(g)
         sol.multiplier_lr_scheduler.step()
+
+    def _scalar_mult_step(self, noise):
+        """Scalar-multiplier branch of SSAC.multiplier_loss / update_multiplier
+        (src/ssac.py:529-578 with mlp_multiplier=False): lam_loss = -softplus(m) *
+        mean(clamp(Qc(s, a) - threshold, lb, ub)), a ~ pi(s); plain Adam, no clip, no
+        schedule. One forward launch, one head launch summing the penalty, and the
+        optimizer launch forms d/dm = -sigmoid(m) * sum / rows on the device."""
+        sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
+        L = _lib.lib()
+        ws = self.ws
+        dist = sol.distributional_qc
+        qshape = (B,) if C == 1 else (B, C)
+        e7 = self._eps('e7', noise.std_normal((B, A)))
+        if dist:
+            noise.randn_like(qshape, used=False)
+        ctr = noise.next()
+        a = self.buf('m.a', B, A)
+        self._run_multi('m.f1s' + noise_tag(e7), lambda: [
+            with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A,
+                      e7, SITE_PI_MULT, a=a)], ctr)
+        self._run_multi('m.f2s', lambda: [
+            fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True)], ctr)
+        aqc = self.buf('m.aqc', B)
+        self._cc_head(ws['m.cc.mu'], ws['m.cc.ls'], aqc, dist)
+        psum = self._loss_slots(1)
+        _lib.check(L.drpo_multiplier_head(B, None, None, aqc.data_ptr(), float(sol.constraint_threshold),
+                                          float(sol.penalty_lb), float(sol.penalty_ub), 0.0, 0.0, None,
+                                          psum.data_ptr(), _lib.stream()), 'multiplier_head')
+        self.dp.sum_(psum)
+        opt = sol.multiplier_optimizer
+        fused_step([opt.segment(0, 1, opt.step_scalars(), grad_from_sum=(psum, B * self.dp.world),
+                                grad_from_sum_kind=1)])
 
     # ------------------------------------------------------------------
     def update_solver(self, alg, update_actor, update_multiplier, noise):

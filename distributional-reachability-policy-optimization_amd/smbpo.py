@@ -399,6 +399,10 @@ class SMBPO(Configurable, Module):
             if cfg.mlp_multiplier:
                 log.message(f'Average Lambda {which}: {mean_lam}')
                 self.data.append(f'Average Lambda {which}', mean_lam)
+        if not cfg.mlp_multiplier:
+            mean_lam = self.solver.lam.item()
+            log.message(f'Average Lambda: {mean_lam}')
+            self.data.append('Average Lambda', mean_lam)
         if torch.cuda.is_available():
             t = torch.cuda.get_device_properties(0).total_memory
             r, a = torch.cuda.memory_reserved(0), torch.cuda.memory_allocated(0)

@@ -171,9 +171,8 @@ class SSAC(Module):
             setattr(self, k, v)
         if isinstance(self.target_entropy, Optional):
             self.target_entropy = None
-        assert self.constrained_fcn == 'reachability', 'only the reachability certificate is on the hot path'
-        assert self.mlp_multiplier, 'the fused multiplier update implements the MLP multiplier'
-        assert self.autotune_alpha and not self.use_log_alpha_loss
+        assert self.constrained_fcn == 'reachability', \
+            "constrained_fcn='cost' is out of scope (the reachability certificate is the DRPO hot path)"
         self.state_dim, self.action_dim, self.con_dim = state_dim, action_dim, con_dim
         self.horizon = horizon
         self.violation_cost = 0.0
@@ -226,16 +225,26 @@ class SSAC(Module):
         if self.target_entropy is None:
             self.target_entropy = -action_dim
 
+        # multiplier (src/ssac.py:232-252): the state-dependent MLP, or one scalar
+        # parameter (init 10, lambda = softplus) in its own one-element flat group
         mg = FlatGroup('multiplier')
-        mult = MLPMultiplier(self.mlp_multiplier_cfg, state_dim, prefix='lam.')
-        mult.spec.register(mg, 'lam.')
-        mg.allocate('cpu')
-        mult.spec.reference_init(mg, 'lam.')
-        mg.data, mg.grad = mg.data.to(device), mg.grad.to(device)
-        mg.enable_packing(spec_pack_layers(mult.spec, 'lam.'))
-        mult.lam = mult.spec.build(mg, 'lam.')
-        mult.group = mg
-        self.multiplier = mult
+        if self.mlp_multiplier:
+            mult = MLPMultiplier(self.mlp_multiplier_cfg, state_dim, prefix='lam.')
+            mult.spec.register(mg, 'lam.')
+            mg.allocate('cpu')
+            mult.spec.reference_init(mg, 'lam.')
+            mg.data, mg.grad = mg.data.to(device), mg.grad.to(device)
+            mg.enable_packing(spec_pack_layers(mult.spec, 'lam.'))
+            mult.lam = mult.spec.build(mg, 'lam.')
+            mult.group = mg
+            self.multiplier = mult
+        else:
+            mg.add('multiplier', ())
+            mg.allocate(device)
+            mg.data[0] = 10.
+            self.multiplier = torch.nn.Parameter(mg.view('multiplier'), requires_grad=False)
+            self.multiplier.grad = mg.view('multiplier', mg.grad)
+        self.multiplier_group = mg
 
         from .optim import Adam, CosineAnnealingLR
         T = self.updates_per_training
@@ -246,10 +255,14 @@ class SSAC(Module):
         self.actor_safe_optimizer = Adam(self.actor_safe.group, lr=self.actor_lr, weight_decay=1e-4)
         self.actor_safe_lr_scheduler = CosineAnnealingLR(self.actor_safe_optimizer, self.actor_updates_num,
                                                          self.actor_lr_end)
-        self.alpha_optimizer = Adam(None, lr=self.actor_lr, weight_decay=0.0)
-        self.multiplier_optimizer = Adam(mg, lr=self.multiplier_lr, weight_decay=1e-4)
-        self.multiplier_lr_scheduler = CosineAnnealingLR(self.multiplier_optimizer, self.lam_updates_num,
-                                                         self.multiplier_lr_end)
+        self.alpha_optimizer = Adam(None, lr=self.actor_lr, weight_decay=0.0)   # stepped only if autotune_alpha
+        if self.mlp_multiplier:
+            self.multiplier_optimizer = Adam(mg, lr=self.multiplier_lr, weight_decay=1e-4)
+            self.multiplier_lr_scheduler = CosineAnnealingLR(self.multiplier_optimizer, self.lam_updates_num,
+                                                             self.multiplier_lr_end)
+        else:   # plain Adam at a fixed lr (no weight decay, no schedule)
+            self.multiplier_optimizer = Adam(mg, lr=self.multiplier_lr, weight_decay=0.0)
+            self.multiplier_lr_scheduler = None
         self.register_buffer('total_updates', torch.zeros([], device=device))
         self._engine = None
 
@@ -260,6 +273,13 @@ class SSAC(Module):
     @property
     def alpha(self):
         return self.log_alpha.exp()
+
+    @property
+    def lam(self):
+        """softplus(multiplier) of the scalar-multiplier configuration (src/ssac.py:261-265)."""
+        assert not self.mlp_multiplier
+        assert self.multiplier.shape == ()
+        return torch.nn.functional.softplus(self.multiplier.detach())
 
     @property
     def violation_value(self):

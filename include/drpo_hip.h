@@ -309,6 +309,9 @@ int drpo_actor_upstream(int64_t B, int C, int distributional, float std_ratio, f
                         float lam_upper_bound /* > 0: lams holds the MLPMultiplier's raw output x and
                                                  lam = ub/2 (1 + tanh(2x/ub)) (src/ssac.py:107-111) is
                                                  applied here; 0: lams holds lam */,
+                        float fixed_lam, float clamp_lb, float clamp_ub /* lams == NULL (scalar-multiplier
+                                                 solver, mlp_multiplier = False): lam = fixed_lam and the
+                                                 certificate term is clamp(Qc, lb, ub) (src/ssac.py:481-484) */,
                         drpo_stream_t stream);
 
 /* chain rule through rsample/tanh/log_prob to the actor head; alpha-loss sum */
@@ -319,7 +322,9 @@ int drpo_squash_backward(int64_t B, int A, const float* raw, const float* u, con
 /* d alpha_loss / d log_alpha (src/ssac.py:498-501) */
 int drpo_alpha_grad(const float* log_alpha, const float* alpha_sum, int64_t B, float* grad, drpo_stream_t stream);
 
-/* multiplier loss gradient w.r.t. the MLPMultiplier output (src/ssac.py:529-568) */
+/* multiplier loss gradient w.r.t. the MLPMultiplier output (src/ssac.py:529-568). x == NULL
+ * (scalar multiplier, src/ssac.py:564-566): *loss accumulates sum_i clamp(actor_qc_i -
+ * threshold, lb, ub), the penalty sum of -mean(softplus(m) * penalty); gx unused. */
 int drpo_multiplier_head(int64_t B, const float* x, const float* safe_qc, const float* actor_qc, float threshold,
                          float penalty_lb, float penalty_ub, float upper_bound, float lam_epsilon, float* gx,
                          float* loss, drpo_stream_t stream);
@@ -405,6 +410,10 @@ typedef struct {
                                  drpo_squash_backward (src/ssac.py:498-501), so the SAC
                                  temperature needs no separate gradient launch */
   int64_t grad_sum_rows;
+  int grad_from_sum_kind;     /* 0: -exp(p_i) * sum / rows (the SAC temperature, alpha loss);
+                                 1: -sigmoid(p_i) * sum / rows (the scalar Lagrange multiplier,
+                                    -mean(softplus(m) * penalty), src/ssac.py:564-566);
+                                 2: -sum / rows (use_log_alpha_loss, src/ssac.py:499) */
   float grad_scale;           /* gradient multiplier applied before clip and Adam (the clip
                                  norm is that of the scaled gradient): 1/G folds the data-
                                  parallel mean into the step after a SUM all-reduce. 0 is

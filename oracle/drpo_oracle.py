@@ -546,7 +546,8 @@ class SSACOracle:
                       critic_lr=3e-4, critic_lr_end=8e-5, actor_lr=8e-5, actor_lr_end=4e-5,
                       multiplier_lr=3e-4, multiplier_lr_end=1e-5, distributional=True, uncertainty=True,
                       deterministic_backup=False, target_entropy=-float(A), batch_size=256,
-                      updates_per_training=1000, actor_update_interval=2, multiplier_update_interval=5)
+                      updates_per_training=1000, actor_update_interval=2, multiplier_update_interval=5,
+                      mlp_multiplier=True, fixed_multiplier=15.0, autotune_alpha=True, use_log_alpha_loss=False)
         self.c.update(cfg)
         self.C, self.A = C, A
         c = self.c
@@ -652,9 +653,10 @@ class SSACOracle:
         return self._last
 
     def update_actor_and_alpha(self, s, rng):
-        """src/ssac.py:458-527 (reachability, mlp multiplier)."""
+        """src/ssac.py:458-527 (reachability; MLP or scalar multiplier; alpha flags)."""
         C, sr = self.C, self.c['std_ratio']
         dist = self.c['distributional']
+        mlp_mult = self.c['mlp_multiplier']
         mode = 'uncertainty' if dist else 'mean'
         store = {}
 
@@ -666,10 +668,14 @@ class SSACOracle:
             alpha = self.alpha
             unc = torch.mean(alpha.detach() * logp - sa_q)
             aqc = get_qc(cons_critic(Q, 'constraint_critic.', s, a, mode, sr, rng), C)
-            with torch.no_grad():
-                a_safe = policy_mean(Q, 'actor_safe.net.', s)
-                sqc = get_qc(cons_critic(Q, 'constraint_critic.', s, a_safe, mode, sr, rng), C)
-                lams = multiplier(Q, 'multiplier.', s, sqc, self.c['ub'])
+            if mlp_mult:
+                with torch.no_grad():
+                    a_safe = policy_mean(Q, 'actor_safe.net.', s)
+                    sqc = get_qc(cons_critic(Q, 'constraint_critic.', s, a_safe, mode, sr, rng), C)
+                    lams = multiplier(Q, 'multiplier.', s, sqc, self.c['ub'])
+            else:   # src/ssac.py:480-483
+                lams = self.c['fixed_multiplier']
+                aqc = torch.clamp(aqc, min=self.c['penalty_lb'], max=self.c['penalty_ub'])
             store['logp'] = logp.detach()
             return unc + torch.mean(torch.mul(lams, aqc))
 
@@ -682,31 +688,48 @@ class SSACOracle:
             a_s, _, _, _ = policy_rsample(Q, 'actor_safe.net.', s, rng)
             return torch.mean(get_qc(cons_critic(Q, 'constraint_critic.', s, a_s, mode, sr, rng), C))
 
-        # alpha loss (src/ssac.py:498-501); uses log_prob.detach()
-        alpha_grad = -self.alpha * torch.mean(store['logp'] + self.c['target_entropy'])
+        # alpha loss (src/ssac.py:498-501); uses log_prob.detach(); the coefficient is
+        # alpha, or log_alpha itself with use_log_alpha_loss
+        coef = 1.0 if self.c['use_log_alpha_loss'] else self.alpha
+        alpha_grad = -coef * torch.mean(store['logp'] + self.c['target_entropy'])
         _, gs = self._grad(safe_loss, kas)
         clip_grads([ga[k] for k in ka], self.c['grad_norm'])
         lr = self.sched['actor'].lr
         for k in ka:
             adam_update(self.opt['actor'], k, self.P[k], ga[k], lr, 1e-4)
         self.sched['actor'].step()
-        la = self.log_alpha.clone()
-        adam_update(self.opt['alpha'], 'log_alpha', la, alpha_grad.detach().clone(), self.c['actor_lr'], 0)
-        self.log_alpha = la
-        clip_grads([gs[k] for k in kas], self.c['grad_norm'])
+        auto = self.c['autotune_alpha']
+        if auto:
+            la = self.log_alpha.clone()
+            adam_update(self.opt['alpha'], 'log_alpha', la, torch.as_tensor(alpha_grad).detach().clone(),
+                        self.c['actor_lr'], 0)
+            self.log_alpha = la
+        # the reference clips / schedules the safe actor at optimizer index 2, which is
+        # the safe actor only when the alpha optimizer sits at index 1 (src/ssac.py:515-527)
+        if auto:
+            clip_grads([gs[k] for k in kas], self.c['grad_norm'])
         lr = self.sched['actor_safe'].lr
         for k in kas:
             adam_update(self.opt['actor_safe'], k, self.P[k], gs[k], lr, 1e-4)
-        self.sched['actor_safe'].step()
+        if auto:
+            self.sched['actor_safe'].step()
 
     def update_multiplier(self, s, rng):
-        """src/ssac.py:529-578 (mlp multiplier)."""
+        """src/ssac.py:529-578 (MLP or scalar multiplier)."""
         C, sr = self.C, self.c['std_ratio']
         mode = 'uncertainty' if self.c['distributional'] else 'mean'
         with torch.no_grad():
             a, _, _, _ = policy_rsample(self.P, 'actor.net.', s, rng)
             aqc = get_qc(cons_critic(self.P, 'constraint_critic.', s, a, mode, sr, rng), C)
             pen = torch.clamp(aqc - self.c['constraint_threshold'], min=self.c['penalty_lb'], max=self.c['penalty_ub'])
+        if not self.c['mlp_multiplier']:
+            # lam_loss = -mean(softplus(m) * penalty): plain Adam (lr multiplier_lr, no
+            # weight decay), no clip, no schedule (src/ssac.py:564-578)
+            _, gm = self._grad(lambda Q: -torch.mean(torch.mul(F.softplus(Q['multiplier']), pen)), ['multiplier'])
+            adam_update(self.opt['multiplier'], 'multiplier', self.P['multiplier'], gm['multiplier'],
+                        self.c['multiplier_lr'], 0)
+            return
+        with torch.no_grad():
             a_safe = policy_mean(self.P, 'actor_safe.net.', s)
             sqc = get_qc(cons_critic(self.P, 'constraint_critic.', s, a_safe, mode, sr, rng), C)
         ub, le = self.c['ub'], self.c['lam_epsilon']

@@ -60,7 +60,7 @@ def main():
     norm = torch.cat([m.state_normalizer.mean, m.state_normalizer.std])
     bounds = torch.tensor([sol.r_min, sol.r_max], dtype=torch.float64)
     flat = torch.cat([sol.critic_group.data, sol.actor.group.data, sol.actor_safe.group.data,
-                      sol.multiplier.group.data, sol.log_alpha.view(1), m.group.data])
+                      sol.multiplier_group.data, sol.log_alpha.view(1), m.group.data])
 
     def gather(t):
         t = t.detach().cpu().contiguous()

@@ -34,7 +34,7 @@ def main():
     torch.cuda.synchronize()
     s0 = alg.virt_buffer.get('states')[:64].contiguous()
     flat = torch.cat([alg.solver.critic_group.data, alg.solver.actor.group.data, alg.solver.actor_safe.group.data,
-                      alg.solver.multiplier.group.data, alg.solver.log_alpha.view(1)]).contiguous()
+                      alg.solver.multiplier_group.data, alg.solver.log_alpha.view(1)]).contiguous()
     gathered = [torch.empty_like(flat) for _ in range(world)]
     dist.all_gather(gathered, flat)
     states = [torch.empty_like(s0) for _ in range(world)]

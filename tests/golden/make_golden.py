@@ -346,11 +346,15 @@ def solver_lrs(sol):
     return np.array([out['critic'], out['actor'], out['actor_safe'], out['multiplier']], dtype=np.float64)
 
 
-def gen_ssac(out, name, seed, tag, distributional, uncertainty):
+def gen_ssac(out, name, seed, tag, distributional, uncertainty, sac_extra=None):
     cfg = small_config(name, distributional=distributional, uncertainty=uncertainty)
+    if sac_extra:
+        cfg.update({'sac_cfg': dict(sac_extra)})
     alg = build_alg(name, cfg, seed)
     sol = alg.solver
     d = meta(name, cfg, alg)
+    for k, v in (sac_extra or {}).items():
+        d['flag/' + k] = np.array(v)
     rng = np.random.RandomState(seed + 5)
     if uncertainty and not distributional:
         # robust certificate target samples the dynamics model inside update_critic
@@ -383,6 +387,21 @@ def gen_ssac(out, name, seed, tag, distributional, uncertainty):
     d.update(sd_dict(sol, 'sd3/'))
     d['lr3'] = solver_lrs(sol)
     np.savez_compressed(os.path.join(out, f'ssac_{tag}.npz'), **d)
+
+
+# the SSAC configuration branches beside the DRPO default (src/ssac.py:117-161):
+# scalar softplus multiplier, fixed temperature, log-alpha temperature loss
+SOLVER_FLAG_CASES = [
+    ('point-robot', 36, 'scalar_mult_point', True, True, {'mlp_multiplier': False, 'penalty_ub': 1.7}),
+    ('quadrotor', 37, 'scalar_mult_quad', False, False, {'mlp_multiplier': False, 'penalty_lb': 0.1}),
+    ('quadrotor', 38, 'fixed_alpha_quad', True, True, {'autotune_alpha': False}),
+    ('point-robot', 39, 'log_alpha_point', True, True, {'use_log_alpha_loss': True}),
+]
+
+
+def gen_solver_flags(out):
+    for name, seed, tag, dist, unc, extra in SOLVER_FLAG_CASES:
+        gen_ssac(out, name, seed, tag, dist, unc, extra)
 
 
 def gen_smbpo_update(out, name, seed):
@@ -631,6 +650,9 @@ def main():
     if sys.argv[1:] == ['checkpoint']:
         gen_checkpoint(out, 61)
         return
+    if sys.argv[1:] == ['solver_flags']:
+        gen_solver_flags(out)
+        return
     if sys.argv[1:] == ['robust']:
         gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
         gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
@@ -646,6 +668,7 @@ def main():
     gen_ssac(out, 'quadrotor', 33, 'vanilla_quad', False, False)
     gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
     gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
+    gen_solver_flags(out)
     gen_smbpo_update(out, 'point-robot', 41)
     gen_smbpo_update(out, 'quadrotor', 42)
     gen_trainer(out, 55)

@@ -25,6 +25,9 @@ def small_smbpo(d, env, factory=None):
                             'distributional_qc': bool(d['meta/distributional']), 'target_entropy': -2.0,
                             'penalty_lb': -1.0, 'actor_lr': 1e-4},
                 'reward_scale': 2.0, 'alive_bonus': 2.0, 'constraint_offset': 0.5, 'constraint_scale': 10.0})
+    flags = {k[len('flag/'):]: d[k].item() for k in d.files if k.startswith('flag/')}
+    if flags:                          # solver-flag fixtures (make_golden.SOLVER_FLAG_CASES)
+        cfg.update({'sac_cfg': flags})
     return drpo_amd.SMBPO(cfg, factory or (lambda id=None: ENVS[env]()), None, 1, device=DEV)
 
 

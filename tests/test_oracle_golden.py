@@ -141,12 +141,20 @@ def test_rollout(env):
 
 
 def ssac_cfg(d):
-    return dict(batch_size=int(d['meta/sac_batch']), distributional=bool(d['meta/distributional']),
-                uncertainty=bool(d['meta/uncertainty']), target_entropy=-2.0, penalty_lb=-1.0,
-                actor_lr=1e-4, updates_per_training=1 * 2 * 10)
+    c = dict(batch_size=int(d['meta/sac_batch']), distributional=bool(d['meta/distributional']),
+             uncertainty=bool(d['meta/uncertainty']), target_entropy=-2.0, penalty_lb=-1.0,
+             actor_lr=1e-4, updates_per_training=1 * 2 * 10)
+    for k in d.files:                  # solver-flag fixtures (make_golden.SOLVER_FLAG_CASES)
+        if k.startswith('flag/'):
+            c[k[len('flag/'):]] = d[k].item()
+    return c
 
 
-@pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point'])
+SSAC_TAGS = ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point', 'scalar_mult_point',
+             'scalar_mult_quad', 'fixed_alpha_quad', 'log_alpha_point']
+
+
+@pytest.mark.parametrize('tag', SSAC_TAGS)
 def test_ssac_updates(tag):
     d = load_golden(f'ssac_{tag}')
     P0 = sd(d, 'sd0/')
