@@ -134,14 +134,25 @@ def _build(flags, lib, objdir, verbose, jobs):
     return _link(objs, lib, force=bool(todo))
 
 
-def build(verbose=False, jobs=8, variant=None):
+def build(verbose=False, jobs=8, variant=None, defines=(), tag=None):
     """variant='stamps': profiling build with in-kernel s_memtime stamps (-DDRPO_STAMPS)
-    into libdrpo_hip_stamps.so; never loaded by the product."""
+    into libdrpo_hip_stamps.so; never loaded by the product. ``defines`` + ``tag``: an
+    A/B build with extra -D macros into libdrpo_hip[_stamps]_<tag>.so (loaded only via
+    DRPO_LIB_OVERRIDE by the profiling scripts)."""
+    flags = FLAGS + ['-D' + d for d in defines]
+    suffix = f'_{tag}' if tag else ''
     if variant == 'stamps':
-        return _build(FLAGS + ['-DDRPO_STAMPS'], os.path.join(HERE, 'libdrpo_hip_stamps.so'),
-                      os.path.join(HERE, 'build_stamps'), verbose, jobs)
+        return _build(flags + ['-DDRPO_STAMPS'], os.path.join(HERE, f'libdrpo_hip_stamps{suffix}.so'),
+                      os.path.join(HERE, 'build_stamps' + suffix), verbose, jobs)
+    if tag:
+        return _build(flags, os.path.join(HERE, f'libdrpo_hip{suffix}.so'), os.path.join(HERE, 'build' + suffix),
+                      verbose, jobs)
     return _build(FLAGS, LIB, OBJ, verbose, jobs)
 
 
 if __name__ == '__main__':
-    print(build(verbose='-v' in sys.argv, variant='stamps' if '--stamps' in sys.argv else None))
+    # python build_lib.py [--stamps] [--tag NAME -D MACRO ...]
+    a = sys.argv[1:]
+    tag = a[a.index('--tag') + 1] if '--tag' in a else None
+    defs = [a[i + 1] for i, x in enumerate(a) if x == '-D']
+    print(build(verbose='-v' in a, variant='stamps' if '--stamps' in a else None, defines=defs, tag=tag))

@@ -283,7 +283,10 @@ __device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N,
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int col = (wave + NW * c) * 16 + (lane & 15);
-    bv[c] = (bias && col < N) ? gload(bias + col) : 0.f;
+    if (bias && __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)bias))   // LDS-staged
+      bv[c] = col < N ? ((const __attribute__((address_space(3))) float*)(bias))[col] : 0.f;
+    else
+      bv[c] = (bias && col < N) ? gload(bias + col) : 0.f;
   }
 }
 

@@ -422,6 +422,23 @@ __device__ __forceinline__ const float* step_opaque(const float* ptr) {
   return ptr;
 }
 
+// A/B knobs of the persistent kernel (profiles/gpu_ab_persist.sh):
+//  DRPO_PERSIST_KARG  read the per-step pointers / sizes through an opaque kernarg
+//                     pointer at their point of use (scalar loads) instead of holding
+//                     the whole argument block in SGPRs across the loop (SGPR spills)
+//  DRPO_PREFETCH_M1   issue the elite member's first-layer fragments and biases at the
+//                     top of the step, so they arrive while the actor runs
+//  DRPO_ABIAS_LDS     actor biases staged in LDS once per launch (LW variant)
+#ifndef DRPO_PERSIST_KARG
+#define DRPO_PERSIST_KARG 0
+#endif
+#ifndef DRPO_PREFETCH_M1
+#define DRPO_PREFETCH_M1 0
+#endif
+#ifndef DRPO_ABIAS_LDS
+#define DRPO_ABIAS_LDS 0
+#endif
+
 struct PersistArgs {
   int S, A, C, Ha, Hm, B, H, ntiles;
   EnvParams env;
@@ -449,6 +466,57 @@ struct PersistArgs {
   int64_t* base_slot;
   int members[PERSIST_MAX_H];
 };
+
+typedef const __attribute__((address_space(4))) PersistArgs* PersistArgsK;   // scalar (constant) loads
+__device__ __forceinline__ PersistArgsK persist_args() {
+  PersistArgsK q = (PersistArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return q;
+}
+#if DRPO_PERSIST_KARG
+#define PARG(f) (persist_args()->f)
+#else
+#define PARG(f) (p.f)
+#endif
+
+// First layer with K <= 16 (one k-step) whose fragments / biases were loaded ahead
+// (DRPO_PREFETCH_M1): the wave's MAXC blocks, clamped to the last valid block (its
+// duplicate results are discarded by the epilogue).
+template <int NW, int MAXC>
+struct Layer1Frags {
+  f32x4 w[MAXC];
+  float b[MAXC];
+};
+
+template <int NW, int MAXC>
+__device__ __forceinline__ void layer1_prefetch(const float* P, const float* bias, int N, Layer1Frags<NW, MAXC>& f) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NCB = (N + 15) >> 4;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) f.w[c] = load_pk(P, min(wave + NW * c, NCB - 1), 0, 1);
+  load_bias<NW, MAXC>(bias, N, f.b);
+}
+
+template <int NW, int RB, int MAXC, int ACT>
+__device__ __forceinline__ void layer1_run(const float* in, int ldi, const Layer1Frags<NW, MAXC>& f, int N, float* out,
+                                           int ldo) {
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  f32x4 acc[RB][MAXC], a[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    a[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][m], f.w[c][m], acc[rb][c], 0, 0, 0);
+  dense_epilogue<NW, RB, MAXC, ACT>(acc, f.b, N, out, ldo, GSave{nullptr, nullptr, 0, 0});
+}
 
 // This step's Gaussian draws into LDS: recorded (original-row layout) or the step
 // engine's Philox keys with the original row. Threads [first, first + count) work.
@@ -533,7 +601,8 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   float* wl1 = vecs + 256;                  /* LW: actor L1 mirror [16 cb][256] */               \
   float* wl3 = wl1 + 16 * 256;              /* LW: actor head mirror [16 k-steps][256] */        \
   float* wl2 = wl3 + 16 * 256;              /* LW: actor L2 [16 cb][PERSIST_L2_LDS][256] */      \
-  (void)wl1; (void)wl2; (void)wl3;                                                            \
+  float* abl = wl2 + 16 * PERSIST_L2_LDS * 256;   /* LW + DRPO_ABIAS_LDS: ab1 | ab2 | ab3 */      \
+  (void)wl1; (void)wl2; (void)wl3; (void)abl;                                                 \
   (void)h3; (void)dout; (void)lout; (void)act; (void)rew; (void)hval; (void)nz_a; (void)nz_m;    \
   (void)flags; (void)alive; (void)s_nalive; (void)red; (void)v_nm; (void)v_ns; (void)v_lo; (void)v_hi;
   const int tile = blockIdx.x;
@@ -564,6 +633,13 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       const int cb = e / (PERSIST_L2_LDS * 64), r = e - cb * PERSIST_L2_LDS * 64;
       reinterpret_cast<f32x4*>(wl2)[e] = gload(a2 + cb * 16 * 64 + r);
     }
+    if constexpr (DRPO_ABIAS_LDS) {
+      for (int e = tid; e < 256; e += NT) {
+        abl[e] = gload(p.ab1 + e);
+        abl[256 + e] = gload(p.ab2 + e);
+      }
+      if (tid < 2 * A) abl[512 + tid] = gload(p.ab3 + tid);
+    }
   }
 
   // ---- initial states (t = 0): chronological replay index -> physical row -----
@@ -588,21 +664,17 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     int zo = 0, ldx = p.ldx, ldh = p.ldh, ldm = p.ldm, ldss = p.lds;
     asm volatile("" : "+s"(zo), "+s"(ldx), "+s"(ldh), "+s"(ldm), "+s"(ldss));
     PERSIST_LDS_LAYOUT(zo, ldx, ldh, ldm, ldss)
-    const int m = p.members[t];
-    const float* aW2 = step_opaque(p.aW2);
-    const float* ab2 = step_opaque(p.ab2);
-    const float* mW1 = p.mW1 + (size_t)m * p.ms_in;
-    const float* mW2 = p.mW2 + (size_t)m * p.ms_hid;
-    const float* dW1 = p.dW1 + (size_t)m * p.ms_hid;
-    const float* dW2 = p.dW2 + (size_t)m * p.ms_out;
-    const float* lW1 = p.lW1 + (size_t)m * p.ms_hid;
-    const float* lW2 = p.lW2 + (size_t)m * p.ms_out;
-    const float* mb1 = p.mb1 + (size_t)m * Hm;
-    const float* mb2 = p.mb2 + (size_t)m * Hm;
-    const float* db1 = p.db1 + (size_t)m * Hm;
-    const float* db2 = p.db2 + (size_t)m * S1;
-    const float* lb1 = p.lb1 + (size_t)m * Hm;
-    const float* lb2 = p.lb2 + (size_t)m * S1;
+    const int m = PARG(members[t]);
+    const float* aW2 = step_opaque(PARG(aW2));
+    const float* ab2 = step_opaque(PARG(ab2));
+    // the elite member's slices, formed where they are used (PARG: re-read per use)
+#define MW(f, st) (PARG(f) + (size_t)m * PARG(st))
+#define MB(f, n) (PARG(f) + (size_t)m * (n))
+#if DRPO_PREFETCH_M1
+    Layer1Frags<NW, MAXC> m1;
+    const bool m1_pre = S + A <= 16;
+    if (m1_pre) layer1_prefetch<NW, MAXC>(MW(mW1, ms_in), MB(mb1, Hm), Hm, m1);
+#endif
 
     if (t == 2) RSTAMP(0);
     if (t == 2) RSTAMP(1);
@@ -612,14 +684,15 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     int* alive_nxt = (t & 1) ? alive : flags;
     // ---- actor MLP (src/policy.py:61-100) ------------------------------------
     if constexpr (LW) {
-      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 1, 1>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh,
+      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 1, 1>(xin, ldx, S, step_opaque(PARG(aW1)),
+                                                   DRPO_ABIAS_LDS ? abl : step_opaque(PARG(ab1)), Ha, h1, ldh,
                                                    GSave{nullptr, nullptr, 0, 0}, wl1);
       lds_barrier();
       if (t == 2) RSTAMP(2);
-      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 16, PERSIST_L2_LDS>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh,
-                                                                 GSave{nullptr, nullptr, 0, 0}, wl2);
+      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 16, PERSIST_L2_LDS>(h1, ldh, Ha, aW2, DRPO_ABIAS_LDS ? abl + 256 : ab2,
+                                                                 Ha, h2, ldh, GSave{nullptr, nullptr, 0, 0}, wl2);
     } else {
-      tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(p.aW1), step_opaque(p.ab1), Ha, h1, ldh);
+      tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(PARG(aW1)), step_opaque(PARG(ab1)), Ha, h1, ldh);
       lds_barrier();
       if (t == 2) RSTAMP(2);
       tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
@@ -630,14 +703,19 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     //      the head's split-K partials are reduced by the threads that sample
     //      (one thread per (row, action dim) sums the mu and log-std columns) ----
     {
-      const float* ab3 = step_opaque(p.ab3);
       float bmu = 0.f, braw = 0.f;
       if (tid < ROWS * A) {   // ROWS * A <= NT (A <= 8)
         const int d = tid % A;
-        bmu = gload(ab3 + d);
-        braw = gload(ab3 + A + d);
+        if constexpr (LW && DRPO_ABIAS_LDS) {
+          bmu = abl[512 + d];
+          braw = abl[512 + A + d];
+        } else {
+          const float* ab3 = step_opaque(PARG(ab3));
+          bmu = gload(ab3 + d);
+          braw = gload(ab3 + A + d);
+        }
       }
-      tile_dense_narrow_partials<NW, RB, LW>(h2, ldh, Ha, step_opaque(p.aW3), red, wl3);
+      tile_dense_narrow_partials<NW, RB, LW>(h2, ldh, Ha, step_opaque(PARG(aW3)), red, wl3);
       if (tid < ROWS * A) {
         const int r = tid / A, d = tid - r * A;
         const float mu = narrow_sum<NW, RB>(red, r, d) + bmu;
@@ -656,12 +734,20 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     if (t == 2) RSTAMP(4);
 
     // ---- elite member forward (src/dynamics.py:112-122) -----------------------
-    tile_dense<NW, RB, MAXC, ACT_SILU>(xin, ldx, S + A, mW1, mb1, Hm, h1, ldh);
+#if DRPO_PREFETCH_M1
+    if (m1_pre) layer1_run<NW, RB, MAXC, ACT_SILU>(xin, ldx, m1, Hm, h1, ldh);
+    else
+#endif
+    tile_dense<NW, RB, MAXC, ACT_SILU>(xin, ldx, S + A, MW(mW1, ms_in), MB(mb1, Hm), Hm, h1, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(5);
-    tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, mW2, mb2, Hm, h2, ldh);
+    tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, MW(mW2, ms_hid), MB(mb2, Hm), Hm, h2, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(6);
+    const float* dW1 = MW(dW1, ms_hid);
+    const float* lW1 = MW(lW1, ms_hid);
+    const float* db1 = MB(db1, Hm);
+    const float* lb1 = MB(lb1, Hm);
     if (paired) {
       tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
       lds_barrier();
@@ -671,10 +757,10 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       float bd = 0.f, bl = 0.f;
       if (tid < ROWS * S1) {   // ROWS * S1 <= NT (S1 <= 16)
         const int j = tid % S1;
-        bd = gload(db2 + j);
-        bl = gload(lb2 + j);
+        bd = gload(MB(db2, S1) + j);
+        bl = gload(MB(lb2, S1) + j);
       }
-      tile_dense_narrow_pair_partials<NW, RB>(h1, h3, ldh, Hm, dW2, lW2, red);
+      tile_dense_narrow_pair_partials<NW, RB>(h1, h3, ldh, Hm, MW(dW2, ms_out), MW(lW2, ms_out), red);
       if (tid < ROWS * S1) {
         const int r = tid / S1, j = tid - r * S1;
         const float mean = (narrow_pair_sum<NW, RB>(red, 0, r, j) + bd) + (j < S ? sraw[r * ldss + j] : 0.f);
@@ -695,8 +781,13 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         if (t == 2) RSTAMP(7);
         // one block per wave: a ring as deep as K (every fragment in flight at once), else
         // this latency-bound layer waits one L2 round trip per few k-steps
-        tile_dense_pair2<NW, RB, 1, ACT_NONE, 13, 13>(h1, h3, ldh, dW2, db2, S1, dout, lW2, lb2, S1, lout, ldm);
+        tile_dense_pair2<NW, RB, 1, ACT_NONE, 13, 13>(h1, h3, ldh, MW(dW2, ms_out), MB(db2, S1), S1, dout,
+                                                       MW(lW2, ms_out), MB(lb2, S1), S1, lout, ldm);
       } else {
+        const float* dW2 = MW(dW2, ms_out);
+        const float* lW2 = MW(lW2, ms_out);
+        const float* db2 = MB(db2, S1);
+        const float* lb2 = MB(lb2, S1);
         tile_dense<NW, RB, MAXC, ACT_SILU>(h2, ldh, Hm, dW1, db1, Hm, h1, ldh);
         lds_barrier();
         if (S1 <= 16) tile_dense_narrow<NW, RB, ACT_NONE>(h1, ldh, Hm, dW2, db2, S1, dout, ldm, red);
@@ -734,14 +825,14 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       if (tid < ROWS && alive_cur[tid]) {
         float hh[8];
         env_constraints_row(p.env, xin + tid * ldx, dn, vl, hh);
-        for (int c = 0; c < C; ++c) p.st_h[(sb + tid) * C + c] = hh[c];
-        p.st_r[sb + tid] = rew[tid];
-        p.st_dv[sb + tid] = (uint8_t)((dn ? 1 : 0) | (vl ? 2 : 0));
+        for (int c = 0; c < C; ++c) PARG(st_h)[(sb + tid) * C + c] = hh[c];
+        PARG(st_r)[sb + tid] = rew[tid];
+        PARG(st_dv)[sb + tid] = (uint8_t)((dn ? 1 : 0) | (vl ? 2 : 0));
         in_r = true;
       }
       const uint64_t mk = __ballot(in_r);
-      if (in_r) p.inv[((size_t)t * p.ntiles + tile) * ROWS + __popcll(mk & ((1ull << tid) - 1ull))] = tid;
-      if (tid == 0) p.cnt[(size_t)t * p.ntiles + tile] = __popcll(mk);
+      if (in_r) PARG(inv)[((size_t)t * PARG(ntiles) + tile) * ROWS + __popcll(mk & ((1ull << tid) - 1ull))] = tid;
+      if (tid == 0) PARG(cnt)[(size_t)t * PARG(ntiles) + tile] = __popcll(mk);
       const uint64_t still = __ballot(in_r && !dn);
       if (tid < ROWS) alive_nxt[tid] = in_r && !dn;
       if (tid == 0) *s_nalive = __popcll(still);
@@ -752,28 +843,30 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
         const int r = e / S, k = e - r * S;
         const float x = xin[r * ldx + k];
         if (alive_cur[r]) {
-          p.st_s[(sb + r) * S + k] = sraw[r * ldss + k];
-          p.st_s2[(sb + r) * S + k] = x;
+          PARG(st_s)[(sb + r) * S + k] = sraw[r * ldss + k];
+          PARG(st_s2)[(sb + r) * S + k] = x;
         }
         sraw[r * ldss + k] = x;   // same element, same thread
       }
       for (int e = ts; e < nrows * A; e += NS) {
         const int r = e / A, d = e - r * A;
-        if (alive_cur[r]) p.st_a[(sb + r) * A + d] = act[r * 8 + d];
+        if (alive_cur[r]) PARG(st_a)[(sb + r) * A + d] = act[r * 8 + d];
       }
-    } else if (t + 1 < p.H) {
-      persist_noise<ROWS>(p.eps_a, p.eps_m, p.seed, p.ctr, A, S1, B, t + 1, row0, nrows, nz_a, nz_m, NT / 2, NT / 2);
+    } else if (t + 1 < PARG(H)) {
+      persist_noise<ROWS>(PARG(eps_a), PARG(eps_m), PARG(seed), PARG(ctr), A, S1, B, t + 1, row0, nrows, nz_a, nz_m, NT / 2, NT / 2);
     }
     lds_barrier();
     if (t == 2) RSTAMP(9);
     const int n_alive = __builtin_amdgcn_readfirstlane(*s_nalive);   // uniform exit
     if (n_alive == 0) {   // the whole tile finished: later steps see no rows from it
-      for (int t2 = t + 1 + tid; t2 < p.H; t2 += NT) p.cnt[(size_t)t2 * p.ntiles + tile] = 0;
+      for (int t2 = t + 1 + tid; t2 < PARG(H); t2 += NT) PARG(cnt)[(size_t)t2 * PARG(ntiles) + tile] = 0;
       break;
     }
   }
 }
 
+#undef MW
+#undef MB
 #undef PERSIST_LDS_LAYOUT
 
 // per step t: exclusive prefix of the tile counts -> pos[t][tile], n[t]
@@ -1086,7 +1179,7 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   const size_t lds_bytes = persist_lds_bytes(S, A, d->Ha, d->Hm, rpt, nw);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
   // LDS-resident actor weights (see rollout_persist_kernel) when they fit
-  const size_t lw_bytes = sizeof(float) * (size_t)(32 + 16 * PERSIST_L2_LDS) * 256;
+  const size_t lw_bytes = sizeof(float) * ((size_t)(32 + 16 * PERSIST_L2_LDS) * 256 + (DRPO_ABIAS_LDS ? 528 : 0));
   const bool lw = rpt == 16 && NW == 8 && S <= 16 && d->Ha == 256 && 2 * A <= 16 && lds_bytes + lw_bytes <= 160 * 1024 &&
                   !getenv("DRPO_ROLLOUT_NO_LDS_WEIGHTS");
   static const bool scan_emit = getenv("DRPO_ROLLOUT_SCAN_EMIT") != nullptr;   // A/B: the two-launch tail

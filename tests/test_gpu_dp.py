@@ -20,7 +20,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize('tag', ['drpo_quad', 'robust_point'])
+@pytest.mark.parametrize('tag', ['drpo_quad', 'robust_point', 'scalar_mult_point', 'log_alpha_point'])
 def test_sac_data_parallel_two_ranks(tag):
     port = _port()
     procs = []
