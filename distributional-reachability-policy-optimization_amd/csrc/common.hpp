@@ -339,6 +339,18 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Wave-local LDS hand-off: a wave reads back, in another lane mapping, values that it
+// wrote itself (a layer's own output columns as the A operand of a split-K head). A
+// wave's LDS operations complete in order, so waiting for its own writes
+// (lgkmcnt(0)) suffices; the memory clobbers keep the compiler from moving the reads
+// above the writes (per thread the addresses differ, so nothing else orders them).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Core of tile_dense_impl for a wave that owns exactly MAXC valid column blocks
 // (the dispatcher below picks the instantiation per wave).
 // NL > 0 (unrolled cores only): the first NL k-steps of every column block are read

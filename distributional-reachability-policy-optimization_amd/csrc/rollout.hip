@@ -430,7 +430,7 @@ __device__ __forceinline__ const float* step_opaque(const float* ptr) {
 //                     top of the step, so they arrive while the actor runs
 //  DRPO_ABIAS_LDS     actor biases staged in LDS once per launch (LW variant)
 #ifndef DRPO_PERSIST_KARG
-#define DRPO_PERSIST_KARG 0
+#define DRPO_PERSIST_KARG 1   // config 2: 248 -> 242 us per launch (profiles/r03/ab_persist)
 #endif
 #ifndef DRPO_PREFETCH_M1
 #define DRPO_PREFETCH_M1 0
@@ -516,6 +516,131 @@ __device__ __forceinline__ void layer1_run(const float* in, int ldi, const Layer
       for (int rb = 0; rb < RB; ++rb)
         acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][m], f.w[c][m], acc[rb][c], 0, 0, 0);
   dense_epilogue<NW, RB, MAXC, ACT>(acc, f.b, N, out, ldo, GSave{nullptr, nullptr, 0, 0});
+}
+
+// The dynamics model's two hidden heads and their narrow output layers
+// (src/dynamics.py:84-91, 112-122) as ONE phase. Waves [0, NW/2) run the diff head's
+// hidden layer, waves [NW/2, NW) the log-var head's: wave w owns blocks base, base + NW/2,
+// ... with base = w (diff) or NW-1-w (log-var), which for 13 blocks per head on 8 waves
+// puts 7 / 6 / 6 / 7 blocks on the four SIMDs. Each wave then forms its split-K share of
+// its head's output layer from exactly the columns it produced (read back from LDS by the
+// same wave: no workgroup barrier between the two layers), the output layer's fragments
+// issued before the hidden epilogue. Partials land in red slot [head][w mod NW/2], the
+// layout narrow_pair_sum reduces.
+template <int NW, int RB, int NC, int NK>
+__device__ __forceinline__ void pair_split_core(int base, const float* in, int ldi, const float* __restrict__ P,
+                                                const float* __restrict__ bias, int N, float* out, int ldo,
+                                                const float* __restrict__ Pn, float* red_slot) {
+  constexpr int HW = NW / 2;
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  int cbs[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) cbs[c] = base + HW * c;
+  f32x4 acc[RB][NC];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int PF = pf_depth<NC>();
+  f32x4 bq[PF][NC];
+#pragma unroll
+  for (int u = 0; u < PF - 1; ++u)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bq[u][c] = load_pk(P, cbs[c], u < NK ? u : NK - 1, NK);
+  float bvs[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = cbs[c] * 16 + l15;
+    bvs[c] = col < N ? gload(bias + col) : 0.f;
+  }
+  f32x4 an[RB], ac[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 4 * g);
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    if (s + PF - 1 < NK) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) bq[(s + PF - 1) % PF][c] = load_pk(P, cbs[c], s + PF - 1, NK);
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) ac[rb] = an[rb];
+    if (s + 1 < NK) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        an[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * ldi + 16 * (s + 1) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF][c][m], acc[rb][c], 0, 0, 0);
+  }
+  // the output layer's k-steps == this wave's hidden column blocks (K = N = Hm)
+  f32x4 nb[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) nb[c] = load_pk(Pn, 0, cbs[c], NK);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = cbs[c] * 16 + l15;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float y = act_fn<ACT_SILU>(acc[rb][c][r] + bvs[c]);
+        out[(rb * 16 + 4 * g + r) * ldo + col] = col < N ? y : 0.f;
+      }
+  }
+  wave_lds_sync();
+  f32x4 pacc[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) pacc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(out + (rb * 16 + l15) * ldo + 16 * cbs[c] + 4 * g);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) pacc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], nb[c][m], pacc[rb], 0, 0, 0);
+    }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red_slot[rb * 256 + (4 * g + r) * 16 + l15] = pacc[rb][r];
+}
+
+template <int NW, int RB, int NC, int NK>
+__device__ __forceinline__ void pair_split_nc(int nc, int base, const float* in, int ldi, const float* P,
+                                              const float* bias, int N, float* out, int ldo, const float* Pn,
+                                              float* red_slot) {
+  if (nc == NC) pair_split_core<NW, RB, NC, NK>(base, in, ldi, P, bias, N, out, ldo, Pn, red_slot);
+  else if constexpr (NC > 1) pair_split_nc<NW, RB, NC - 1, NK>(nc, base, in, ldi, P, bias, N, out, ldo, Pn, red_slot);
+}
+
+// in: the trunk output (K = N = Hm, NK k-steps); out1 / out2: the heads' hidden
+// activations; Pn1 / Pn2: the output layers (Hm -> S+1 <= 16). Ends with the barrier
+// that publishes the partials.
+template <int NW, int RB, int MAXC, int NK>
+__device__ __forceinline__ void pair_split_heads(const float* in, int ldi, int N, const float* P1, const float* b1,
+                                                 float* out1, const float* Pn1, const float* P2, const float* b2,
+                                                 float* out2, const float* Pn2, float* red) {
+  constexpr int HW = NW / 2;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool second = wave >= HW;
+  const int base = second ? NW - 1 - wave : wave;
+  const int NCB = (N + 15) >> 4;
+  const int nc = base < NCB ? min(MAXC, (NCB - base + HW - 1) / HW) : 0;
+  float* slot = red + (size_t)((second ? HW : 0) + (second ? wave - HW : wave)) * RB * 256;
+  if (nc > 0)
+    pair_split_nc<NW, RB, MAXC, NK>(nc, base, in, ldi, second ? P2 : P1, second ? b2 : b1, N, second ? out2 : out1,
+                                    ldi, second ? Pn2 : Pn1, slot);
+  else {   // a wave without blocks contributes zero partials
+    const int lane = threadIdx.x & 63;
+    for (int e = lane; e < RB * 256; e += 64) slot[e] = 0.f;
+  }
+  lds_barrier();
 }
 
 // This step's Gaussian draws into LDS: recorded (original-row layout) or the step
@@ -697,7 +822,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       if (t == 2) RSTAMP(2);
       tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
     }
-    lds_barrier();
+    // the head's split-K share of wave w is k-steps w, w + NW, ...: exactly the hidden
+    // column blocks wave w just wrote (Ha <= 256), so no workgroup barrier here
+    wave_lds_sync();
     if (t == 2) RSTAMP(3);
     // ---- actor head + squashed Gaussian sample + model input [normalize(s), a]:
     //      the head's split-K partials are reduced by the threads that sample
@@ -749,18 +876,19 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     const float* db1 = MB(db1, Hm);
     const float* lb1 = MB(lb1, Hm);
     if (paired) {
-      tile_dense_pair<NW, RB, PMAXC, ACT_SILU, 13>(h2, ldh, Hm, dW1, db1, Hm, h1, lW1, lb1, Hm, h3, ldh);
-      lds_barrier();
-      if (t == 2) RSTAMP(7);
-      // output heads (split-K partials) reduced by the threads that form the
-      // residual mean, soft-clamp the log-variance and sample the next state
+      // output-layer biases first (their latency hides behind the hidden layers)
       float bd = 0.f, bl = 0.f;
       if (tid < ROWS * S1) {   // ROWS * S1 <= NT (S1 <= 16)
         const int j = tid % S1;
         bd = gload(MB(db2, S1) + j);
         bl = gload(MB(lb2, S1) + j);
       }
-      tile_dense_narrow_pair_partials<NW, RB>(h1, h3, ldh, Hm, MW(dW2, ms_out), MW(lW2, ms_out), red);
+      // both hidden heads + their output layers' split-K partials, one barrier
+      pair_split_heads<NW, RB, (13 + NW / 2 - 1) / (NW / 2), 13>(h2, ldh, Hm, dW1, db1, h1, MW(dW2, ms_out), lW1,
+                                                                 lb1, h3, MW(lW2, ms_out), red);
+      if (t == 2) RSTAMP(7);
+      // the partials reduced by the threads that form the residual mean, soft-clamp the
+      // log-variance and sample the next state
       if (tid < ROWS * S1) {
         const int r = tid / S1, j = tid - r * S1;
         const float mean = (narrow_pair_sum<NW, RB>(red, 0, r, j) + bd) + (j < S ? sraw[r * ldss + j] : 0.f);
