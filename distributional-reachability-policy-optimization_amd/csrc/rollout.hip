@@ -706,13 +706,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   float* h2 = h1 + ROWS * (LDH);                                                              \
   float* h3 = h2 + ROWS * (LDH);                                                              \
   float* sraw = h3 + ROWS * (LDH);           /* ROWS x lds  states at the start of the step */  \
-  float* ao = sraw + ROWS * (LDSS);          /* ROWS x 20   actor head */                       \
-  float* dout = ao + ROWS * 20;                                                               \
+  float* dout = sraw + ROWS * (LDSS);       /* ROWS x ldm  (tracking's output layers) */        \
   float* lout = dout + ROWS * (LDM);                                                          \
   float* act = lout + ROWS * (LDM);          /* ROWS x 8 */                                     \
   float* rew = act + ROWS * 8;                                                                \
-  float* hval = rew + ROWS;                  /* ROWS x 8 */                                     \
-  float* nz_a = hval + ROWS * 8;             /* ROWS x 8    this step's action draws */         \
+  float* nz_a = rew + ROWS;                  /* ROWS x 8    this step's action draws */         \
   float* nz_m = nz_a + ROWS * 8;             /* ROWS x 64   this step's model draws */          \
   int* flags = reinterpret_cast<int*>(nz_m + ROWS * 64);                                      \
   int* alive = flags + ROWS;                                                                  \
@@ -728,7 +726,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   float* wl2 = wl3 + 16 * 256;              /* LW: actor L2 [16 cb][PERSIST_L2_LDS][256] */      \
   float* abl = wl2 + 16 * PERSIST_L2_LDS * 256;   /* LW + DRPO_ABIAS_LDS: ab1 | ab2 | ab3 */      \
   (void)wl1; (void)wl2; (void)wl3; (void)abl;                                                 \
-  (void)h3; (void)dout; (void)lout; (void)act; (void)rew; (void)hval; (void)nz_a; (void)nz_m;    \
+  (void)h3; (void)dout; (void)lout; (void)act; (void)rew; (void)nz_a; (void)nz_m;    \
   (void)flags; (void)alive; (void)s_nalive; (void)red; (void)v_nm; (void)v_ns; (void)v_lo; (void)v_hi;
   const int tile = blockIdx.x;
   const int row0 = tile * ROWS;
@@ -1254,11 +1252,14 @@ static int hb_for(int64_t n) {
 }
 
 // LDS bytes of rollout_persist_kernel for `rpt`-row tiles (without the LDS-resident
-// actor weights)
+// actor weights): per row xin, h1-h3, sraw, dout, lout, act, rew, nz_a, nz_m, flags,
+// alive; then s_nalive, the split-K partials and the normalizer / log-var vectors.
+// (Tracking, S = 51: 162.7 KB at 32-row tiles, inside the 160 KiB, so B >= 8192 runs
+// 32-row tiles there too.)
 static size_t persist_lds_bytes(int S, int A, int Ha, int Hm, int rpt, int nw) {
   const int S1 = S + 1;
   const int ldx = lds_ld(S + A), ldh = lds_ld(Ha > Hm ? Ha : Hm), ldm = round_up(S1, 16) + 4, ldss = round_up(S, 4);
-  return sizeof(float) * ((size_t)rpt * (ldx + 3 * ldh + ldss + 20 + 2 * ldm + 8 + 1 + 8 + 8 + 64 + 2) + 4 +
+  return sizeof(float) * ((size_t)rpt * (ldx + 3 * ldh + ldss + 2 * ldm + 8 + 1 + 8 + 64 + 2) + 4 +
                           (size_t)nw * (rpt / 16) * 256 + 256);
 }
 
@@ -1381,8 +1382,10 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
   RolloutWs w = rollout_ws(d->B, d->S, d->H, (char*)d->workspace);
   // 32-row tiles halve the weight bytes per MFMA once the batch fills the chip with
   // them (B >= 8192), when the wider tile still fits the LDS (not for tracking's S=51)
+  static const bool force16 = getenv("DRPO_ROLLOUT_RPT16") != nullptr;   // A/B
   const int rpt = d->rows_per_tile ? d->rows_per_tile
-                                   : (d->B >= 256 * 32 && persist_lds_bytes(d->S, d->A, d->Ha, d->Hm, 32, 8) <= 160 * 1024
+                                   : (!force16 && d->B >= 256 * 32 &&
+                                              persist_lds_bytes(d->S, d->A, d->Ha, d->Hm, 32, 8) <= 160 * 1024
                                           ? 32 : 16);
   DRPO_REQUIRE(rpt == 16 || rpt == 32, "drpo_rollout: rows_per_tile must be 16 or 32");
   const int S = d->S, A = d->A, S1 = d->S + 1;
