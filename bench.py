@@ -28,6 +28,7 @@ ranks); sac.value = SAC grad-steps/s over the update phases. ms_per_step is the
 full rollout_and_update wall time (max over ranks).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -358,10 +359,31 @@ def main():
     sync_parameters(alg)            # every rank starts from rank 0's weights (DP replicas)
     do_sac = not args.rollout_only
 
-    roll_ms, sac_ms, kern_ms = [], [], []
+    roll_ms, sac_ms, kern_ms, call_ms = [], [], [], []
     n_dev = torch.zeros(1, dtype=torch.int64, device=dev)
 
+    from drpo_amd import _lib as dlib
+    # production noise: ops.rollout picks the fused engine (2) for H <= 128
+    fused_engine = args.engine == 2 or (args.engine == 0 and H <= 128)
+    fused_engine = fused_engine and os.environ.get('DRPO_BENCH_TORCH_PHASE') != '1'   # A/B: torch phase events
+
     def one_step(tmr):
+        if tmr is not None and fused_engine:
+            # Fused engine: the library records tmr.events[0] immediately before the
+            # persist kernel (the rollout's first GPU work) and events[1] after it, so
+            # events[0] opens the rollout phase, and events[2] / [3] (free: one kernel
+            # pair) close it and the SAC phase. The phase spans the same GPU work as a
+            # separate event recorded before the call, minus that event's own gap.
+            # events[4]: before the Python call (the call-bracketed figure, reported beside)
+            dlib.check(dlib.lib().drpo_event_record(tmr.events[4], dlib.stream()), 'event_record')
+            out = alg.rollout(alg.actor, timer=tmr)
+            dlib.check(dlib.lib().drpo_event_record(tmr.events[2], dlib.stream()), 'event_record')
+            if do_sac:
+                for st in range(alg.solver_updates_per_step):
+                    alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
+            dlib.check(dlib.lib().drpo_event_record(tmr.events[3], dlib.stream()), 'event_record')
+            n_dev.add_(out._count)
+            return None
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
         t2 = torch.cuda.Event(enable_timing=True)
@@ -384,7 +406,7 @@ def main():
     n_dev.zero_()
     # no host synchronisation inside the timed region: the host enqueues ahead of the
     # GPU, so the per-phase event intervals are GPU time, not host launch latency
-    timers = [EventTimer(2 * H) for _ in range(args.steps)]
+    timers = [EventTimer(max(5, 2 * H)) for _ in range(args.steps)]
     wall0 = time.perf_counter()
     evs = [one_step(timers[i]) for i in range(args.steps)]
     torch.cuda.synchronize()
@@ -393,19 +415,29 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - wall0
     for e, tmr in zip(evs, timers):
-        roll_ms.append(e[0].elapsed_time(e[1]))
-        sac_ms.append(e[1].elapsed_time(e[2]))
+        if e is None:   # fused engine: library events (see one_step)
+            ph = tmr.elapsed_pairs(2)  # (ev0, ev1) = kernel; (ev2, ev3) = SAC phase
+            rs = ctypes.c_float()
+            dlib.check(dlib.lib().drpo_event_elapsed_ms(ctypes.byref(rs), tmr.events[0], tmr.events[2]), 'elapsed')
+            roll_ms.append(rs.value)
+            sac_ms.append(ph[1])
+            dlib.check(dlib.lib().drpo_event_elapsed_ms(ctypes.byref(rs), tmr.events[4], tmr.events[2]), 'elapsed')
+            call_ms.append(rs.value)
+        else:
+            roll_ms.append(e[0].elapsed_time(e[1]))
+            sac_ms.append(e[1].elapsed_time(e[2]))
         kern_ms.extend(tmr.elapsed_pairs(getattr(tmr, 'pairs', H)))
     n_trans = int(n_dev.item())
-    tot = torch.tensor([wall, sum(roll_ms) / 1e3, sum(sac_ms) / 1e3, float(n_trans)], dtype=torch.float64, device=dev)
+    tot = torch.tensor([wall, sum(roll_ms) / 1e3, sum(sac_ms) / 1e3, float(n_trans), sum(call_ms) / 1e3],
+                       dtype=torch.float64, device=dev)
     if dist is not None:
         mx = tot.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tot.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        wall, roll_s, sac_s, n_all = mx[0].item(), mx[1].item(), mx[2].item(), sm[3].item()
+        wall, roll_s, sac_s, n_all, call_s = mx[0].item(), mx[1].item(), mx[2].item(), sm[3].item(), mx[4].item()
     else:
-        wall, roll_s, sac_s, n_all = tot[0].item(), tot[1].item(), tot[2].item(), tot[3].item()
+        wall, roll_s, sac_s, n_all, call_s = tot[0].item(), tot[1].item(), tot[2].item(), tot[3].item(), tot[4].item()
 
     # post-pass (untimed): per-kernel-class MLP throughput of the SAC update from HIP
     # events around every MLP launch (drpo_amd.sac_step.LaunchProfiler). Every rank
@@ -490,6 +522,12 @@ def main():
                 if do_sac and sac_s > 0 else None,
                 'mlp_kernels': sac_kernels},
         'model_fit': fit_res,
+        # the rollout phase behind `value`: device time from the library's event right before
+        # the persist kernel to the event after the emit (the rollout's own GPU work); the
+        # call-bracketed figure starts at an event recorded before the Python call instead
+        'rollout_phase': {'bounds': 'library events around the rollout kernels' if call_ms else 'torch events around the call',
+                          'ms_per_rollout': roll_s / args.steps * 1e3,
+                          'value_call_bracketed': (n_all / call_s) if call_ms and call_s > 0 else None},
         'roofline': {'kernel': kname, 'bound': 'mfma', 'achieved': achieved,
                      'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_PEAK_TFLOPS,
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,
