@@ -686,7 +686,10 @@ __device__ __forceinline__ void persist_noise(const float* eps_a, const float* e
 // Ha == 256, 2A <= 16 and the LDS to spare (host check).
 constexpr int PERSIST_L2_LDS = 3;
 
-template <int RB, int NW, bool LW>
+// PM: the dynamics heads' path fixed at compile time (1: paired heads, S+1 <= 16 and
+// Hm = 200; 0: the general path; -1: chosen at run time), so a specialised kernel holds
+// registers for one path only
+template <int RB, int NW, bool LW, int PM = -1>
 __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p) {
   constexpr int ROWS = RB * 16;
   constexpr int NT = NW * 64;
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   const int row0 = tile * ROWS;
   const int nrows = min(ROWS, B - row0);
   const int Ha = p.Ha, Hm = p.Hm;
-  const bool paired = S1 <= 16 && Hm == 200;
+  const bool paired = PM >= 0 ? PM == 1 : (S1 <= 16 && Hm == 200);
   {
   PERSIST_LDS_LAYOUT(0, p.ldx, p.ldh, p.ldm, p.lds)
   if (tid < 256) {
@@ -1311,6 +1314,8 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   const size_t lw_bytes = sizeof(float) * ((size_t)(32 + 16 * PERSIST_L2_LDS) * 256 + (DRPO_ABIAS_LDS ? 528 : 0));
   const bool lw = rpt == 16 && NW == 8 && S <= 16 && d->Ha == 256 && 2 * A <= 16 && lds_bytes + lw_bytes <= 160 * 1024 &&
                   !getenv("DRPO_ROLLOUT_NO_LDS_WEIGHTS");
+  const bool paired = S1 <= 16 && d->Hm == 200;   // the kernel's PM specialisation
+  static const bool pm_rt = getenv("DRPO_ROLLOUT_PM_RUNTIME") != nullptr;   // A/B: unspecialised kernels
   static const bool scan_emit = getenv("DRPO_ROLLOUT_SCAN_EMIT") != nullptr;   // A/B: the two-launch tail
   const bool self_emit = (int64_t)H * a.ntiles <= EMIT_SELF_MAX && !scan_emit;
   if (self_emit) {
@@ -1319,11 +1324,23 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   }
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
   if (rpt == 32)
-    rollout_persist_kernel<2, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+  {
+    if (pm_rt)
+      rollout_persist_kernel<2, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+    else if (paired)
+      rollout_persist_kernel<2, 8, false, 1><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+    else
+      rollout_persist_kernel<2, 8, false, 0><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+  }
   else if (NW == 16)
     rollout_persist_kernel<1, 16, false><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);
   else if (lw)
-    rollout_persist_kernel<1, 8, true><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
+  {
+    if (paired && !pm_rt)
+      rollout_persist_kernel<1, 8, true, 1><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
+    else
+      rollout_persist_kernel<1, 8, true><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
+  }
   else
     rollout_persist_kernel<1, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   DRPO_LAUNCH_CHECK("rollout_persist");
