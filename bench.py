@@ -24,7 +24,9 @@ rows with gradients all-reduced over RCCL (weak scaling); config 5 divides its
 global batch over the ranks instead (strong scaling).
 
 value = imagined transitions/s over the rollout phases of the timed region (all
-ranks); sac.value = SAC grad-steps/s over the update phases. ms_per_step is the
+ranks), each phase bracketed by events recorded right before and right after the
+SMBPO.rollout() call (transitions written by one rollout / its
+time); sac.value = SAC grad-steps/s over the update phases. ms_per_step is the
 full rollout_and_update wall time (max over ranks).
 """
 import argparse
@@ -443,15 +445,21 @@ def main():
     # events around every MLP launch (drpo_amd.sac_step.LaunchProfiler). Every rank
     # runs it (the updates all-reduce gradients); rank 0 reports.
     sac_kernels = None
+    sac_comm = None
     if do_sac:
         from drpo_amd.sac_step import LaunchProfiler
+        from drpo_amd.distributed import CommLog
         eng = alg.solver.engine
         eng.profiler = LaunchProfiler()
+        CommLog.timing, c0 = [], CommLog.calls      # HIP events around every gradient exchange
         for st in range(alg.solver_updates_per_step):
             alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
         torch.cuda.synchronize()
         summ = eng.profiler.summarise()
         eng.profiler = None
+        sac_comm = {'ms_per_update': CommLog.take_ms() / alg.solver_updates_per_step,
+                    'collectives_per_update': (CommLog.calls - c0) / alg.solver_updates_per_step}
+        CommLog.timing = None
         sac_kernels = {k: {'tflops': round(v['tflops'], 2), 'frac': round(v['tflops'] / FP32_PEAK_TFLOPS, 4),
                            'avg_launch_us': round(v['avg_ms'] * 1e3, 2), 'launches': v['launches']}
                        for k, v in summ.items() if ':' not in k}
@@ -477,6 +485,13 @@ def main():
         if dist is not None:
             dist.all_reduce(fit_s, op=dist.ReduceOp.MAX)
         fit_s = fit_s.item()
+        # communication share of a fit step (untimed post-pass, events around each exchange)
+        from drpo_amd.distributed import CommLog
+        CommLog.timing, c0 = [], CommLog.calls
+        m.fit(alg.replay_buffer, steps=50)
+        torch.cuda.synchronize()
+        fit_comm = {'ms_per_step': CommLog.take_ms() / 50, 'collectives_per_step': (CommLog.calls - c0) / 50}
+        CommLog.timing = None
         from drpo_amd.distributed import member_sharding
         sh = member_sharding(m)
         fl = fit_flop_per_step(S, A, E, m.batch_size, m.hidden_dim)
@@ -484,7 +499,7 @@ def main():
                    'fit_steps_per_s': args.fit_steps / fit_s, 'flop_per_fit_step': fl,
                    'achieved_tflops_job': fl * args.fit_steps / fit_s / 1e12,
                    'frac_job': fl * args.fit_steps / fit_s / 1e12 / (FP32_PEAK_TFLOPS * world),
-                   'rows_per_step': E * m.batch_size,
+                   'rows_per_step': E * m.batch_size, 'comm': fit_comm,
                    'sharding': f'members {sh.ranges}' if sh is not None else
                    ('batch (gradient all-reduce)' if world > 1 else 'single')}
         steady_mode(alg)
@@ -500,9 +515,13 @@ def main():
     rows_per_launch = n_trans / max(1, len(kern_ms))
     achieved = flop_tr * rows_per_launch / (k_avg_ms * 1e-3) / 1e12
     sac_flop = sac_flop_per_step(B, S, A, C)
+    # headline: the call-bracketed rollout phase (events before / after SMBPO.rollout());
+    # the phase that starts at the library's own event before the persist kernel is
+    # reported beside it as rollout_phase.kernel_bounded
+    head_s = call_s if call_ms else roll_s
     res = {
         'metric': METRIC,
-        'value': n_all / roll_s,
+        'value': n_all / head_s,
         'unit': 'imagined transitions/s',
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': wall / args.steps * 1e3,
@@ -515,19 +534,25 @@ def main():
                 'value': (alg.solver_updates_per_step * args.steps / sac_s) if do_sac and sac_s > 0 else None,
                 'rank_steps_per_s': (alg.solver_updates_per_step * args.steps / sac_s) if do_sac and sac_s > 0
                 else None,
-                'global_batch': B * world, 'gradient_exchange': 'RCCL all-reduce (mean) per optimizer group'
+                'global_batch': B * world, 'gradient_exchange': 'one RCCL sum all-reduce bucket per optimizer '
+                'phase (critic | actor + safe actor + alpha sum | multiplier), 1/G in the optimizer'
                 if world > 1 else None,
                 'flop_per_step_per_rank': sac_flop, 'measured': do_sac,
                 'achieved_tflops_per_gpu': (sac_flop * alg.solver_updates_per_step * args.steps / sac_s / 1e12)
                 if do_sac and sac_s > 0 else None,
-                'mlp_kernels': sac_kernels},
+                'mlp_kernels': sac_kernels,
+                # gradient exchanges per update_solver (untimed post-pass, HIP events around each)
+                'comm': sac_comm},
         'model_fit': fit_res,
-        # the rollout phase behind `value`: device time from the library's event right before
-        # the persist kernel to the event after the emit (the rollout's own GPU work); the
-        # call-bracketed figure starts at an event recorded before the Python call instead
-        'rollout_phase': {'bounds': 'library events around the rollout kernels' if call_ms else 'torch events around the call',
-                          'ms_per_rollout': roll_s / args.steps * 1e3,
-                          'value_call_bracketed': (n_all / call_s) if call_ms and call_s > 0 else None},
+        # the rollout phase behind `value`: from an event recorded before the Python call to
+        # one recorded after it returns; kernel_bounded starts at the library's own event
+        # right before the persist kernel instead (the rollout's GPU work only)
+        'rollout_phase': {'bounds': 'events before / after the SMBPO.rollout() call',
+                          'ms_per_rollout': head_s / args.steps * 1e3,
+                          'kernel_bounded': {'value': n_all / roll_s, 'ms_per_rollout': roll_s / args.steps * 1e3,
+                                             'bounds': 'library event before the persist kernel -> event after '
+                                                       'the call'} if call_ms else None,
+                          'call_over_kernel_bounded': (call_s / roll_s) if call_ms and roll_s > 0 else None},
         'roofline': {'kernel': kname, 'bound': 'mfma', 'achieved': achieved,
                      'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_PEAK_TFLOPS,
                      'traffic': None, 'avg_launch_ms': k_avg_ms, 'flop_per_transition': flop_tr,

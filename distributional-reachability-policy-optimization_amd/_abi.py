@@ -145,14 +145,14 @@ class MlpBwdNet(ctypes.Structure):
 class MlpBwd(ctypes.Structure):
     """drpo_mlp_bwd_t"""
     _fields_ = [('net', MlpBwdNet * 3), ('nnets', c_int), ('trunk', c_int), ('rows', c_int64), ('nbatch', c_int),
-                ('split_heads', c_int)]
+                ('split_heads', c_int), ('upstream', c_int)]
 
 
 class WgradItem(ctypes.Structure):
     """drpo_wgrad_item_t"""
     _fields_ = [('dz', P), ('y', P), ('gW', P), ('gb', P), ('dout', c_int), ('din', c_int), ('rows', c_int64),
                 ('zstride', c_int64), ('ystride', c_int64), ('gwstride', c_int64), ('gbstride', c_int64),
-                ('nbatch', c_int)]
+                ('nbatch', c_int), ('sq', P), ('sq_off', c_int)]
 
 
 class BufferView(ctypes.Structure):
@@ -174,10 +174,13 @@ class CriticHead(ctypes.Structure):
 PROTOTYPES.update({
     'drpo_mlp_forward': (c_int, [POINTER(MlpFwd), P]),
     'drpo_mlp_forward_multi': (c_int, [POINTER(MlpFwd), P, c_int, c_uint64, c_uint64, P]),
+    'drpo_mlp_backward_multi_head': (c_int, [POINTER(MlpBwd), P, c_int, POINTER(CriticHead), P]),
     'drpo_mlp_backward_multi': (c_int, [POINTER(MlpBwd), P, c_int, P]),
     'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
-    'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P]),
-    'drpo_mlp_wgrad_reduce': (c_int, [POINTER(WgradItem), c_int, POINTER(EnsReduce), P]),
+    'drpo_mlp_wgrad_workspace_size': (c_size_t, [POINTER(WgradItem), c_int]),
+    'drpo_mlp_wgrad_tiles': (c_int, [POINTER(WgradItem)]),
+    'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P, c_size_t, P]),
+    'drpo_mlp_wgrad_reduce': (c_int, [POINTER(WgradItem), c_int, POINTER(EnsReduce), P, c_size_t, P]),
     'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
                                   c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
     'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,

@@ -3,6 +3,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include "common.hpp"
 
 static thread_local char g_err[1024] = "";
@@ -19,10 +21,15 @@ DRPO_API const char* drpo_last_error(void) { return g_err; }
 DRPO_API int drpo_version(void) { return 1; }
 
 // HIP event helpers so hosts without a HIP binding (ctypes/cgo/JNI) can time
-// individual kernels on the stream they run on.
+// individual kernels on the stream they run on. The events are timing-only: created
+// without the system-scope release a default event record carries (measured: a
+// default timing event left the GPU idle ~5.7 us per record between two kernels,
+// profiles/r04a), since nothing reads memory through them. DRPO_EVENT_SYSTEM_FENCE=1
+// restores the default (A/B).
 DRPO_API int drpo_event_create(void** ev) {
   hipEvent_t e;
-  hipError_t r = hipEventCreate(&e);
+  static const bool sys_fence = getenv("DRPO_EVENT_SYSTEM_FENCE") != nullptr;
+  hipError_t r = sys_fence ? hipEventCreate(&e) : hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   if (r != hipSuccess) {
     drpo_set_error("hipEventCreate: %s", hipGetErrorString(r));
     return DRPO_EHIP;

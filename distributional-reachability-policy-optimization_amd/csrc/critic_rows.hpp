@@ -1,0 +1,74 @@
+// Per-row math of the safe-SAC critic losses (src/ssac.py:284-435), shared by the
+// stand-alone drpo_critic_head kernel (csrc/sac.hip) and the critic backward launch,
+// which forms its own output gradients from the forward outputs (no separate head
+// launch on the production path, csrc/mlp.hip).
+#pragma once
+#include "common.hpp"
+
+namespace drpo {
+
+__device__ __forceinline__ float sp_grad(float x) { return x > 20.f ? 1.f : 1.f / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float cc_std(float l, float lmin, float lmax) {
+  float ls = lmax - softplusf(lmax - l);
+  ls = lmin + softplusf(ls - lmin);
+  return expf(ls);
+}
+
+// d std / d raw for std = exp(lmin + sp(lmax - sp(lmax - l) - lmin))
+__device__ __forceinline__ float cc_dstd_draw(float l, float lmin, float lmax, float std) {
+  const float ls1 = lmax - softplusf(lmax - l);
+  return std * sp_grad(ls1 - lmin) * sp_grad(lmax - l);
+}
+
+// The head descriptor may be referenced from the kernarg segment (address space 4:
+// scalar loads) or from generic memory, hence the template parameter.
+// soft Bellman target of row i with the twin-min target critics (src/ssac.py:284-294)
+template <typename Head>
+__device__ __forceinline__ float critic_target(const Head& p, int64_t i, float alpha) {
+  float nv = fminf(p.q0t[i], p.q1t[i]);
+  if (!p.deterministic_backup) nv = nv - alpha * p.logp2[i];
+  const float dn = p.d[i] ? 1.f : 0.f;
+  return p.r[i] + p.discount * (1.f - dn) * nv;
+}
+
+// certificate element k = (i, c): reachability backup (src/ssac.py:304-413), the
+// distributional (3-term) or MSE loss term (src/ssac.py:415-435) and its gradients
+// w.r.t. the mean / raw log-std head outputs. Returns the loss term (already / (B C)).
+template <typename Head>
+__device__ __forceinline__ float cert_element(const Head& p, int64_t i, int c, float& dmu, float& dls) {
+  const int64_t k = i * p.C + c;
+  const float invN = 1.f / (float)(p.B * p.C);
+  const float dn = p.d[i] ? 1.f : 0.f;
+  // certificate-target done flags: the batch's, or the model-predicted ones of the
+  // robust branch (src/ssac.py:387-400)
+  const float dnc = p.dc ? (p.dc[i] ? 1.f : 0.f) : dn;
+  const float hv = p.h[k];
+  const float mu = p.mu[k];
+  float q2;
+  if (p.distributional) {
+    const float e = fminf(fmaxf(normal_at(p.eps3, k, p.seed, p.ctr, 7u), -2.f), 2.f);
+    q2 = p.mu_t[k] + e * cc_std(p.ls_t[k], p.lmin, p.lmax);
+  } else {
+    q2 = p.mu_t[k];
+  }
+  const float nonterm = (1.f - p.discount) * hv + p.discount * fmaxf(hv, q2);
+  const float yc = nonterm * (1.f - dnc) + hv * dnc;
+  if (p.distributional) {
+    const float diff = fminf(fmaxf(yc - mu, -p.qc_td_bound), p.qc_td_bound);
+    const float yb = diff + mu;
+    const float sd = cc_std(p.ls[k], p.lmin, p.lmax);
+    const float var = sd * sd;
+    const float t1 = (mu - yc) * (mu - yc) / (2.f * var);
+    const float t2 = (mu - yb) * (mu - yb) / (2.f * var);
+    dmu = (mu - yc) / var * invN;
+    const float dsd = (-(mu - yb) * (mu - yb) / (var * sd) + 1.f / sd) * invN;
+    dls = dsd * cc_dstd_draw(p.ls[k], p.lmin, p.lmax, sd);
+    return (t1 + t2 + logf(sd)) * invN;
+  }
+  dmu = 2.f * (mu - yc) * invN;
+  dls = 0.f;
+  return (mu - yc) * (mu - yc) * invN;
+}
+
+}  // namespace drpo

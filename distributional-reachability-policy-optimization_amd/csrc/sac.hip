@@ -19,12 +19,11 @@
 // Losses are accumulated (already scaled) with float atomics into caller-zeroed
 // device scalars, so no host synchronisation is needed.
 #include "common.hpp"
+#include "critic_rows.hpp"
 
 using namespace drpo;
 
 namespace {
-
-__device__ __forceinline__ float sp_grad(float x) { return x > 20.f ? 1.f : 1.f / (1.f + expf(-x)); }
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -38,18 +37,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;   // valid in thread 0
 }
 
-
-__device__ __forceinline__ float cc_std(float l, float lmin, float lmax) {
-  float ls = lmax - softplusf(lmax - l);
-  ls = lmin + softplusf(ls - lmin);
-  return expf(ls);
-}
-
-// d std / d raw for std = exp(lmin + sp(lmax - sp(lmax - l) - lmin))
-__device__ __forceinline__ float cc_dstd_draw(float l, float lmin, float lmax, float std) {
-  const float ls1 = lmax - softplusf(lmax - l);
-  return std * sp_grad(ls1 - lmin) * sp_grad(lmax - l);
-}
 
 }  // namespace
 
@@ -222,48 +209,15 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float lq = 0.f, lc = 0.f;
   if (i < p.B) {
-    // soft Bellman target (src/ssac.py:284-294)
-    const float alpha = expf(*p.log_alpha);
-    float nv = fminf(p.q0t[i], p.q1t[i]);
-    if (!p.deterministic_backup) nv = nv - alpha * p.logp2[i];
-    const float dn = p.d[i] ? 1.f : 0.f;
-    // certificate-target done flags: the batch's, or the model-predicted ones of the
-    // robust branch (src/ssac.py:387-400)
-    const float dnc = p.dc ? (p.dc[i] ? 1.f : 0.f) : dn;
-    const float y = p.r[i] + p.discount * (1.f - dn) * nv;
+    const float y = critic_target(p, i, expf(*p.log_alpha));
     const float e0 = p.q0[i] - y, e1 = p.q1[i] - y;
     const float invB = 1.f / (float)p.B;
     lq = (e0 * e0 + e1 * e1) * (0.5f * invB);
-    const float invN = 1.f / (float)(p.B * p.C);
     for (int c = 0; c < p.C; ++c) {
-      const int64_t k = i * p.C + c;
-      const float hv = p.h[k];
-      const float mu = p.mu[k];
-      float q2;
-      if (p.distributional) {
-        const float e = fminf(fmaxf(normal_at(p.eps3, k, p.seed, p.ctr, 7u), -2.f), 2.f);
-        q2 = p.mu_t[k] + e * cc_std(p.ls_t[k], p.lmin, p.lmax);
-      } else {
-        q2 = p.mu_t[k];
-      }
-      const float nonterm = (1.f - p.discount) * hv + p.discount * fmaxf(hv, q2);
-      const float yc = nonterm * (1.f - dnc) + hv * dnc;
-      if (p.distributional) {
-        const float diff = fminf(fmaxf(yc - mu, -p.qc_td_bound), p.qc_td_bound);
-        const float yb = diff + mu;
-        const float sd = cc_std(p.ls[k], p.lmin, p.lmax);
-        const float var = sd * sd;
-        const float t1 = (mu - yc) * (mu - yc) / (2.f * var);
-        const float t2 = (mu - yb) * (mu - yb) / (2.f * var);
-        lc += (t1 + t2 + logf(sd)) * invN;
-        p.dmu[k] = (mu - yc) / var * invN;
-        const float dsd = (-(mu - yb) * (mu - yb) / (var * sd) + 1.f / sd) * invN;
-        p.dls[k] = dsd * cc_dstd_draw(p.ls[k], p.lmin, p.lmax, sd);
-      } else {
-        lc += (mu - yc) * (mu - yc) * invN;
-        p.dmu[k] = 2.f * (mu - yc) * invN;
-        if (p.dls) p.dls[k] = 0.f;
-      }
+      float dmu, dls;
+      lc += cert_element(p, i, c, dmu, dls);
+      p.dmu[i * p.C + c] = dmu;
+      if (p.dls) p.dls[i * p.C + c] = dls;
     }
     // the critic gradients are stored after the certificate loop: a store ahead of
     // the loop's loads would cost the row a second memory latency

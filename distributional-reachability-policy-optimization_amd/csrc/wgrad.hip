@@ -1,0 +1,496 @@
+// Grouped weight gradients dW = dZ^T Y, db = colsum(dZ) for every layer of a
+// parameter group in ONE launch (the reference's autograd of BatchedLinear /
+// nn.Linear, src/dynamics.py:26-52, src/torch_util.py:190-211), plus the per-tile
+// sums of squares of the finished gradient that clip_grad_norm_ needs
+// (src/ssac.py:454,494-527, torch.nn.utils.clip_grad_norm_).
+//
+// Work split. An item (one layer x nbatch members) is cut into output tiles of
+// TO x TI (TO, TI = 64, or 16 for a layer with <= 16 outputs / inputs, so the
+// narrow output heads and the S+A-wide input layers do not pay for 64-wide
+// padding) times row chunks. One 256-thread workgroup owns a (tile, chunk) unit:
+// its 4 waves split the chunk's rows (4-row k-groups, interleaved), and every wave
+// streams its own dZ / Y fragments straight from global memory into a register ring
+// (no LDS staging, no barriers in the main loop): per k-group one 16-byte load of 4
+// consecutive outputs and one of 4 consecutive inputs feed 4 x 4 MFMAs
+// (v_mfma_f32_16x16x4_f32, exact f32), MFMA m covering o = o0 + 4*(lane&15) + m and
+// MFMA n covering i = i0 + 4*(lane&15) + n, k = the 4 rows. The chunk sizes are
+// chosen on the host so that every unit costs about the same and all units are
+// resident at once (<= 2 workgroups per CU): no partial second round.
+//
+// Hand-off. The 4 waves' partial tiles are summed through LDS. A tile with one row
+// chunk adds its sum to the gradient directly. Otherwise each unit writes its partial
+// (and bias partial) to a slab with write-through (sc1) stores, waits for them
+// (vmcnt(0)), and one lane adds 1 to the tile's arrival counter (agent-scope atomic).
+// The workgroup whose add returns nch-1 is the last: it resets the counter, loads
+// every slab of the tile with sc1 loads, sums them in chunk order (deterministic, no
+// float atomics), adds the sum to the gradient and writes the tile's sum of squares.
+// That is MI355X_MICROARCH.md's validated hand-off (sc1 payload, drained, one
+// ticket add per workgroup, last arriver by the returned value, sc1 loads); nothing
+// ever waits, so no schedule can hang it.
+#include "common.hpp"
+#include "ens_reduce.hpp"
+
+using namespace drpo;
+
+namespace {
+constexpr int WG_NW = 4;                 // waves per workgroup
+constexpr int WG_NT = WG_NW * 64;
+constexpr int WG_D = 5;                  // register ring slots (k-groups of 4 rows each)
+constexpr int WG_ROWQ = 64;              // chunk granularity (rows)
+constexpr int WG_MAXITEMS = 16;
+constexpr int WG_SLD = 264;              // LDS slab stride per accumulator block (== 8 mod 32)
+}  // namespace
+
+struct WgradPlan {
+  int to, ti;              // tile shape (64 or 16)
+  int nto, nti, nch;       // tiles along outputs / inputs, row chunks
+  int chunk;               // rows per chunk (multiple of WG_ROWQ)
+  int va, vb;              // 16-byte loads of dZ / Y rows (widths % 4 == 0, aligned)
+  int64_t first_unit;      // first logical workgroup of the item
+  int64_t first_tile;      // first arrival counter of the item
+  int64_t slab_off;        // first slab float of the item (tiles with nch > 1)
+};
+
+struct WgradArgs {
+  drpo_wgrad_item_t it[WG_MAXITEMS];
+  WgradPlan pl[WG_MAXITEMS];
+  int64_t units;
+  int n;
+  int has_red;
+  drpo_ens_reduce_t red;
+  float* slab;
+  unsigned* ctr;
+};
+
+// write-through (sc1) float store / load: the slab hand-off between workgroups
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 4 consecutive columns c..c+3 (W == 4) or column c (W == 1, in .x) of row `row` of a
+// row-major [.][ld] matrix. No value is masked here: the caller clamps row / c to
+// valid addresses, a column past the matrix only feeds output elements that are never
+// stored, and rows past the chunk are zeroed where the fragment is consumed (a
+// select right after the load would make the wave wait for it, collapsing the ring).
+template <int W, bool VEC>
+__device__ __forceinline__ f32x4 frag_load(const float* __restrict__ M, int64_t row, int64_t ld, int c, int ncols) {
+  const float* p = M + row * ld + c;
+  f32x4 v;
+  if constexpr (W == 4 && VEC) {
+    v = gload(reinterpret_cast<const f32x4*>(p));
+  } else if constexpr (W == 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = gload(c + u < ncols ? p + u : p);
+  } else {
+    v = f32x4{gload(p), 0.f, 0.f, 0.f};
+  }
+  return v;
+}
+
+template <int TO, int TI>
+__device__ __forceinline__ void frag_mma(const f32x4& a, const f32x4& b, f32x4 (&acc)[TO / 16][TI / 16]) {
+  constexpr int MA = TO / 16, MB = TI / 16;
+  if constexpr (MA == 4 && MB == 4) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], b[n], acc[m][n], 0, 0, 0);
+  } else if constexpr (MA == 4) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], b[0], acc[m][0], 0, 0, 0);
+  } else if constexpr (MB == 4) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[0][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[n], acc[0][n], 0, 0, 0);
+  } else {
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], acc[0][0], 0, 0, 0);
+  }
+}
+
+// LDS float index, inside wave w's slab, of tile element (ol, il) (accumulator
+// layout: acc[m][n][rr] of lane (G, L) holds o = 4*(4G + rr) + m (TO 64) or
+// 4G + rr (TO 16), i = 4L + n (TI 64) or L (TI 16))
+template <int TO, int TI>
+__device__ __forceinline__ int slab_index(int w, int ol, int il) {
+  constexpr int NA = (TO / 16) * (TI / 16), NB = TI / 16;
+  int m, rr, G, n, L;
+  if constexpr (TO == 64) {
+    m = ol & 3; rr = (ol >> 2) & 3; G = ol >> 4;
+  } else {
+    m = 0; rr = ol & 3; G = ol >> 2;
+  }
+  if constexpr (TI == 64) {
+    n = il & 3; L = il >> 2;
+  } else {
+    n = 0; L = il;
+  }
+  return (w * NA + m * NB + n) * WG_SLD + rr * 64 + 16 * G + L;
+}
+
+__device__ __forceinline__ float wg_block_sum(float v, float* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < WG_NW; ++i) s += red[i];
+  return s;   // valid in thread 0
+}
+
+template <int TO, int TI, bool VA, bool VB>
+__device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u, float* lds) {
+  constexpr int MA = TO / 16, MB = TI / 16, NA = MA * MB;
+  constexpr int WA = TO == 64 ? 4 : 1, WB = TI == 64 ? 4 : 1;
+  constexpr int E = TO * TI / WG_NT;          // tile elements per thread (16, 4 or 1)
+  const drpo_wgrad_item_t& I = a.it[q];
+  const WgradPlan& P = a.pl[q];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l15 = lane & 15;
+  const int it_i = (int)(u % P.nti);
+  int64_t rest = u / P.nti;
+  const int it_o = (int)(rest % P.nto);
+  rest /= P.nto;
+  const int ch = (int)(rest % P.nch);
+  const int zb = (int)(rest / P.nch);
+  const int64_t tile_local = ((int64_t)zb * P.nto + it_o) * P.nti + it_i;
+  const int dout = I.dout, din = I.din;
+  const float* __restrict__ dz = I.dz + (size_t)zb * I.zstride;
+  const float* __restrict__ y = I.y + (size_t)zb * I.ystride;
+  const int o0 = it_o * TO, i0 = it_i * TI;
+  const int64_t r0 = (int64_t)ch * P.chunk;
+  const int64_t r1 = min(I.rows, r0 + P.chunk);
+  const bool do_bias = it_i == 0;
+
+  // this lane's columns, clamped to valid addresses (masked to zero when out of range)
+  const int ca_raw = o0 + (WA == 4 ? 4 * l15 : l15);
+  const int cb_raw = i0 + (WB == 4 ? 4 * l15 : l15);
+  const int ca = ca_raw < dout ? ca_raw : 0, cb = cb_raw < din ? cb_raw : 0;
+
+  f32x4 acc[MA][MB];
+#pragma unroll
+  for (int m = 0; m < MA; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
+
+  // wave k-group j covers rows r0 + 16 j + 4 wave + (0..3); lane group g takes row 4.. + g
+  const int nj = P.chunk / (4 * WG_NW);      // k-groups per wave
+  const int64_t rlane = r0 + 4 * wave + g;
+  auto ld = [&](int j, f32x4& fa, f32x4& fb) {
+    const int64_t r = rlane + 16 * (int64_t)j;
+    const int64_t rc = r < r1 ? r : r1 - 1;
+    fa = frag_load<WA, VA>(dz, rc, dout, ca, dout);
+    fb = frag_load<WB, VB>(y, rc, din, cb, din);
+  };
+  auto use = [&](int j, f32x4 fa, const f32x4& fb) {
+    if (rlane + 16 * (int64_t)j >= r1) fa = f32x4{0.f, 0.f, 0.f, 0.f};   // row past the chunk
+    frag_mma<TO, TI>(fa, fb, acc);
+    if (do_bias) bsum += fa;
+  };
+  // Register ring of WG_D slots: step s loads k-group s into slot s % D and consumes
+  // k-group s - (D - 1) (D - 1 k-groups of cover). Every load is inside the loop: with
+  // a prologue of loads outside it the compiler drains vmcnt at every loop entry. Steps
+  // past the chunk load clamped rows that are never consumed or are zeroed at use.
+  f32x4 ra[WG_D], rb[WG_D];
+#pragma unroll
+  for (int v = 0; v < WG_D; ++v) ra[v] = rb[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int steps = (nj + WG_D - 1 + WG_D - 1) / WG_D * WG_D;
+  for (int s0 = 0; s0 < steps; s0 += WG_D) {
+#pragma unroll
+    for (int v = 0; v < WG_D; ++v) {
+      ld(s0 + v, ra[v], rb[v]);
+      // keep the prefetch here: the scheduler would otherwise sink the loads past the
+      // MFMAs, next to their first use
+      __builtin_amdgcn_sched_barrier(0);
+      if (s0 + v >= WG_D - 1) use(s0 + v - (WG_D - 1), ra[(v + 1) % WG_D], rb[(v + 1) % WG_D]);
+    }
+  }
+
+  // the 4 waves' partial tiles -> LDS slabs (conflict-free: lanes write consecutive words)
+  float* R = lds;
+#pragma unroll
+  for (int m = 0; m < MA; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) R[(wave * NA + m * MB + n) * WG_SLD + rr * 64 + lane] = acc[m][n][rr];
+  // bias partials: sum over the 4 row lanes g of each column, then over waves (LDS)
+  float* Rb = lds + WG_NW * NA * WG_SLD;      // [WG_NW][TO]
+  if (do_bias) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float s = bsum[c];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      bsum[c] = s;
+    }
+    if (g == 0) {
+      if constexpr (WA == 4) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) Rb[wave * TO + 4 * l15 + c] = bsum[c];
+      } else {
+        Rb[wave * TO + l15] = bsum[0];
+      }
+    }
+  }
+  __syncthreads();
+  // thread t owns tile elements t + 256 e: il = t % TI, ol = t / TI + (256 / TI) e
+  float pv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = tid + WG_NT * e;
+    const int ol = idx / TI, il = idx % TI;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WG_NW; ++w) s += R[slab_index<TO, TI>(w, ol, il)];
+    pv[e] = s;
+  }
+  float pb = 0.f;
+  if (do_bias && tid < TO) {
+#pragma unroll
+    for (int w = 0; w < WG_NW; ++w) pb += Rb[w * TO + tid];
+  }
+  constexpr int SL = TO * TI + TO;            // slab floats per unit (tile + bias)
+  float* gW = I.gW + (size_t)zb * I.gwstride;
+  float* gb = I.gb + (size_t)zb * I.gbstride;
+  float* red = lds + WG_NW * NA * WG_SLD + WG_NW * TO;   // 4 floats
+  if (P.nch > 1) {
+    float* my = a.slab + P.slab_off + (tile_local * P.nch + ch) * SL;
+#pragma unroll
+    for (int e = 0; e < E; ++e) st_sc1(my + tid + WG_NT * e, pv[e]);
+    if (do_bias && tid < TO) st_sc1(my + TO * TI + tid, pb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int& s_last = *reinterpret_cast<int*>(red + 4);
+    if (tid == 0) {
+      unsigned* c = a.ctr + P.first_tile + tile_local;
+      const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(P.nch - 1);
+      if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // last arriver: the tile's partials in chunk order
+    const float* base = a.slab + P.slab_off + tile_local * P.nch * SL;
+#pragma unroll
+    for (int e = 0; e < E; ++e) pv[e] = 0.f;
+    pb = 0.f;
+    for (int c = 0; c < P.nch; ++c) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) pv[e] += ld_sc1(base + c * SL + tid + WG_NT * e);
+      if (do_bias && tid < TO) pb += ld_sc1(base + c * SL + TO * TI + tid);
+    }
+  }
+  // gradient += sum (the caller's gradient is zeroed or holds terms to accumulate);
+  // every load is issued before the first store
+  float gv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = tid + WG_NT * e;
+    const int o = o0 + idx / TI, i = i0 + idx % TI;
+    gv[e] = (o < dout && i < din) ? gW[(size_t)o * din + i] : 0.f;
+  }
+  const bool bias_mine = do_bias && tid < TO && o0 + tid < dout;
+  const float gbv = bias_mine ? gb[o0 + tid] : 0.f;
+  float sq = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = tid + WG_NT * e;
+    const int o = o0 + idx / TI, i = i0 + idx % TI;
+    if (o < dout && i < din) {
+      const float v = gv[e] + pv[e];
+      gW[(size_t)o * din + i] = v;
+      sq = fmaf(v, v, sq);
+    }
+  }
+  if (bias_mine) {
+    const float v = gbv + pb;
+    gb[o0 + tid] = v;
+    sq = fmaf(v, v, sq);
+  }
+  if (I.sq) {
+    const float s = wg_block_sum(sq, red);
+    if (tid == 0) I.sq[I.sq_off + tile_local] = s;
+  }
+}
+
+template <int TO, int TI>
+__device__ __forceinline__ void wgrad_unit_v(const WgradArgs& a, int q, int64_t u, float* lds) {
+  const WgradPlan& P = a.pl[q];
+  if (P.va && P.vb) wgrad_unit<TO, TI, true, true>(a, q, u, lds);
+  else if (P.va) wgrad_unit<TO, TI, true, false>(a, q, u, lds);
+  else if (P.vb) wgrad_unit<TO, TI, false, true>(a, q, u, lds);
+  else wgrad_unit<TO, TI, false, false>(a, q, u, lds);
+}
+
+__global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  // logical order: item, then (member, chunk, o-tile, i-tile) with i fastest, spread so
+  // that each XCD runs one contiguous range: the units of one row chunk (which read the
+  // same dZ / Y rows) share an L2
+  const int64_t bid = xcd_block().x;
+  if (a.has_red && bid == a.units) {
+    ens_loss_reduce_block(a.red);
+    return;
+  }
+  int q = 0;
+  while (q + 1 < a.n && bid >= a.pl[q + 1].first_unit) ++q;
+  const WgradPlan& P = a.pl[q];
+  const int64_t u = bid - P.first_unit;
+  if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
+  else if (P.to == 64) wgrad_unit_v<64, 16>(a, q, u, wsm);
+  else if (P.ti == 64) wgrad_unit_v<16, 64>(a, q, u, wsm);
+  else wgrad_unit_v<16, 16>(a, q, u, wsm);
+}
+
+// LDS: 4 wave slabs of the largest tile + bias partials + the block-sum scratch
+static size_t wgrad_lds() { return sizeof(float) * ((size_t)WG_NW * 16 * WG_SLD + WG_NW * 64 + 8); }
+
+namespace {
+
+struct Plan {
+  WgradArgs a;
+  int64_t tiles;     // arrival counters
+  int64_t slab;      // slab floats
+};
+
+int wg_cus() {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return cus;
+}
+
+// per-k-group cost of a tile shape in MFMA-issue units (a 16-MFMA k-group is MFMA
+// bound; the narrow shapes are bound by their 1.25 / 0.5 KB of loads)
+int kg_cost(int to, int ti) { return to == 64 && ti == 64 ? 16 : (to == 64 || ti == 64 ? 6 : 3); }
+
+int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Plan& p) {
+  WgradArgs& a = p.a;
+  a = WgradArgs{};
+  int m = 0;
+  struct Shape { int to, ti, nto, nti; int64_t rows, nb; };
+  Shape sh[WG_MAXITEMS];
+  for (int k = 0; k < n; ++k) {
+    const drpo_wgrad_item_t& I = items[k];
+    DRPO_REQUIRE(I.dz && I.y && I.gW && I.gb && I.dout >= 1 && I.din >= 1 && I.rows >= 0 && I.nbatch >= 1,
+                 "drpo_mlp_wgrad: bad item %d", k);
+    DRPO_REQUIRE(!I.sq || I.sq_off >= 0, "drpo_mlp_wgrad: item %d sq_off", k);
+    for (int j = 0; j < k; ++j)
+      DRPO_REQUIRE(items[j].gW != I.gW, "drpo_mlp_wgrad: items %d and %d write the same gradient", j, k);
+    if (I.rows == 0) continue;
+    a.it[m] = I;
+    Shape& s = sh[m];
+    s.to = I.dout <= 16 ? 16 : 64;
+    s.ti = I.din <= 16 ? 16 : 64;
+    s.nto = (I.dout + s.to - 1) / s.to;
+    s.nti = (I.din + s.ti - 1) / s.ti;
+    s.rows = I.rows;
+    s.nb = I.nbatch;
+    ++m;
+  }
+  a.n = m;
+  // chunk sizes: every unit about the same cost, all units resident at once (<= 2 per CU)
+  const int64_t slots = 2 * (int64_t)wg_cus();
+  auto units_for = [&](double per, int* nch, int* chunk) {
+    int64_t tot = 0;
+    for (int k = 0; k < m; ++k) {
+      const Shape& s = sh[k];
+      const double rows_per = per * 16.0 / kg_cost(s.to, s.ti);   // rows whose cost per wave is `per`
+      int64_t c = (int64_t)((double)s.rows / (rows_per > 1 ? rows_per : 1) + 0.5);
+      c = c < 1 ? 1 : c;
+      int64_t ck = (s.rows + c - 1) / c;
+      ck = (ck + WG_ROWQ - 1) / WG_ROWQ * WG_ROWQ;
+      c = (s.rows + ck - 1) / ck;
+      nch[k] = (int)c;
+      chunk[k] = (int)ck;
+      tot += c * s.nto * s.nti * s.nb;
+    }
+    return tot;
+  };
+  double total = 0;
+  for (int k = 0; k < m; ++k)
+    total += (double)sh[k].nb * sh[k].nto * sh[k].nti * ((sh[k].rows + 15) / 16) * kg_cost(sh[k].to, sh[k].ti);
+  int nch[WG_MAXITEMS], chunk[WG_MAXITEMS];
+  double per = total / (double)slots;
+  if (per < 1) per = 1;
+  // grow the per-unit cost until the units fit the resident slots (one round)
+  for (int it = 0; it < 64 && units_for(per, nch, chunk) > slots; ++it) per *= 1.08;
+  int64_t unit = 0, tile = 0, slab = 0;
+  for (int k = 0; k < m; ++k) {
+    const Shape& s = sh[k];
+    WgradPlan& P = a.pl[k];
+    const drpo_wgrad_item_t& I = a.it[k];
+    P.to = s.to; P.ti = s.ti; P.nto = s.nto; P.nti = s.nti; P.nch = nch[k]; P.chunk = chunk[k];
+    P.va = (I.dout & 3) == 0 && ((uintptr_t)I.dz & 15) == 0 && (I.zstride & 3) == 0;
+    P.vb = (I.din & 3) == 0 && ((uintptr_t)I.y & 15) == 0 && (I.ystride & 3) == 0;
+    P.first_unit = unit;
+    P.first_tile = tile;
+    P.slab_off = slab;
+    const int64_t ntile = (int64_t)s.nto * s.nti * s.nb;
+    unit += ntile * P.nch;
+    tile += ntile;
+    if (P.nch > 1) slab += ntile * P.nch * ((int64_t)s.to * s.ti + s.to);
+  }
+  a.units = unit;
+  p.tiles = tile;
+  p.slab = slab;
+  if (red) {
+    DRPO_REQUIRE(red->part && red->mse && red->Z >= 1 && red->Z <= 256 && red->S1 >= 1 && red->S1 <= LOSS_MAXS1 &&
+                     red->nbx >= 1,
+                 "drpo_mlp_wgrad_reduce: bad reduction");
+    a.has_red = 1;
+    a.red = *red;
+  }
+  return DRPO_OK;
+}
+
+size_t ws_bytes(const Plan& p) { return (size_t)((p.tiles * 4 + 255) / 256 * 256) + sizeof(float) * (size_t)p.slab; }
+
+}  // namespace
+
+DRPO_API int drpo_mlp_wgrad_tiles(const drpo_wgrad_item_t* I) {
+  if (!I || I->dout < 1 || I->din < 1 || I->nbatch < 1) return 0;
+  const int to = I->dout <= 16 ? 16 : 64, ti = I->din <= 16 ? 16 : 64;
+  return ((I->dout + to - 1) / to) * ((I->din + ti - 1) / ti) * I->nbatch;
+}
+
+DRPO_API size_t drpo_mlp_wgrad_workspace_size(const drpo_wgrad_item_t* items, int n) {
+  if (n < 0 || n > WG_MAXITEMS || (n > 0 && !items)) return 0;
+  Plan p;
+  if (plan(items, n, nullptr, p) != DRPO_OK) return 0;
+  return ws_bytes(p);
+}
+
+DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, void* workspace, size_t workspace_bytes,
+                            drpo_stream_t stream) {
+  return drpo_mlp_wgrad_reduce(items, n, nullptr, workspace, workspace_bytes, stream);
+}
+
+DRPO_API int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red,
+                                   void* workspace, size_t workspace_bytes, drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS && (n == 0 || items), "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
+  static Plan p;   // host scratch (the library is driven by one host thread per process)
+  const int rc = plan(items, n, red, p);
+  if (rc != DRPO_OK) return rc;
+  const size_t need = ws_bytes(p);
+  DRPO_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
+               "drpo_mlp_wgrad: workspace %zu bytes < %zu (drpo_mlp_wgrad_workspace_size)", workspace_bytes, need);
+  p.a.ctr = (unsigned*)workspace;
+  p.a.slab = (float*)((char*)workspace + (size_t)((p.tiles * 4 + 255) / 256 * 256));
+  const int64_t blocks = p.a.units + (red ? 1 : 0);
+  if (blocks == 0) return DRPO_OK;
+  mlp_wgrad_kernel<<<(unsigned)blocks, WG_NT, wgrad_lds(), stream>>>(p.a);
+  DRPO_LAUNCH_CHECK("mlp_wgrad");
+  return DRPO_OK;
+}

@@ -4,10 +4,11 @@ One process per GPU (torchrun), ``torch.distributed`` over RCCL/xGMI ("nccl") or
 gloo for the CPU tests. The path shards with ONE exchange per optimizer step:
 
   SAC update   each rank draws its own minibatch shard; after the fused backward
-               + weight-gradient kernels, the flat gradient of the group being
-               stepped (critic+constraint critic 1.37 MB | actor, safe actor and
-               log_alpha | multiplier) is mean-all-reduced, then every rank runs
-               the identical clip + Adam (clip uses the post-reduce norm).
+               + weight-gradient kernels, ONE buffer per optimizer phase is
+               sum-all-reduced (critic + constraint critic 1.37 MB | the actor
+               exchange arena: actor + safe actor gradients + alpha-loss sum,
+               0.56 MB | multiplier), then every rank runs the identical clip + Adam
+               (the 1/G and the clip on the post-reduce norm ride in the optimizer).
   model fit    same for the ensemble's flat group; the holdout MSEs are averaged
                too so every rank picks the same elites.
   rollout      batch-sharded, no communication inside the horizon loop.
@@ -34,6 +35,35 @@ def world_size():
 
 def rank():
     return _dist.get_rank() if is_active() else 0
+
+
+class CommLog:
+    """Process-wide tally of the data-parallel collectives the hot path issues (tests
+    count them per update) and, when ``timing`` is a list, HIP events around each one
+    on the current stream (bench.py reports the communication time per update / fit
+    step from them in an untimed post-pass)."""
+    calls = 0
+    timing = None
+
+    @classmethod
+    def all_reduce(cls, t, group=None):
+        cls.calls += 1
+        if cls.timing is not None and t.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _dist.all_reduce(t, group=group)
+            e1.record()
+            cls.timing.append((e0, e1))
+        else:
+            _dist.all_reduce(t, group=group)
+
+    @classmethod
+    def take_ms(cls):
+        """Sum of the recorded exchange times (ms; call after a synchronize) and reset."""
+        ms = sum(a.elapsed_time(b) for a, b in (cls.timing or []))
+        if cls.timing is not None:
+            cls.timing = []
+        return ms
 
 
 def broadcast_int(value, src=0):
@@ -73,7 +103,7 @@ class GradReducer:
             return
         for t in tensors:
             if t is not None:
-                _dist.all_reduce(t, group=self.group)
+                CommLog.all_reduce(t, group=self.group)
 
     def mean_(self, *tensors):
         if self.world == 1:
@@ -83,7 +113,7 @@ class GradReducer:
         for t in tensors:
             if t is None:
                 continue
-            _dist.all_reduce(t, group=self.group)
+            CommLog.all_reduce(t, group=self.group)
             t.div_(self.world)
 
     def broadcast_(self, *tensors, src=0):
@@ -151,7 +181,7 @@ class MemberShard:
 
     def sum_(self, t):
         if self.world > 1:
-            _dist.all_reduce(t, group=self.group)
+            CommLog.all_reduce(t, group=self.group)
 
     def broadcast_(self, *ts, src=0):
         if self.world > 1:

@@ -54,6 +54,7 @@ class EnsembleEngine:
     def __init__(self, model):
         self.m = model
         self.ws = {}
+        self.wg_ws = {}
         self.noise = None
         self.dev = model.group.data.device
         from .distributed import GradReducer
@@ -244,33 +245,55 @@ class EnsembleEngine:
         return mse, gD, gL
 
     def _backward_descs(self, nets, strides, save_x, gD, gL, b, Z):
+        """Backward-data descriptor and the weight-gradient items: (desc, [(items, n)]).
+        Split heads (DRPO_SPLIT_BWD, an A/B knob) leave the trunk dZ as two terms; the
+        second term's items go in a second launch (one launch never has two items on
+        one gradient)."""
         split = nets[0].dz2[0] is not None
         d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides, split_heads=split)
-        items = []
+        items, extra = [], []
         trunk_out = nets[0].sy[-1]
         for j, net in enumerate(nets):
             ins = [save_x if j == 0 else trunk_out] + [net.sy[l] for l in range(len(net.layers) - 1)]
             for l, (W, bb, din, dout, act, _) in enumerate(net.layers):
                 gW, gb = net.grad_layers[l]
-                # split heads: the trunk dZ is dz + dz2, one item per term, both adding
-                # into the zeroed gradient. Deterministic only while each item is ONE row
-                # chunk (rows <= the wgrad chunk, no split-K): two float adds onto 0
-                # commute, four or more addends do not. Off by default (DRPO_SPLIT_BWD).
-                for dz in (net.dz[l], net.dz2[l]):
+                for dz, dst in ((net.dz[l], items), (net.dz2[l], extra)):
                     if dz is None:
                         continue
                     it = WgradItem()
                     it.dz, it.y, it.gW, it.gb = dz.data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
                     it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
                     it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
-                    items.append(it)
-        return d, (WgradItem * len(items))(*items), len(items)
+                    dst.append(it)
+        launches = [((WgradItem * len(x))(*x), len(x)) for x in (items, extra) if x]
+        return d, launches
+
+    def _wgrad_ws(self, key, arr, n):
+        """Per-call-site weight-gradient workspace (sized once per descriptor array)."""
+        c = self.wg_ws.get(key)
+        if c is not None and c[0] is arr:
+            return c[1]
+        from .sac_step import wgrad_workspace
+        ws = wgrad_workspace(self.ws, f'{key}.wgws', arr, n, self.dev)
+        self.wg_ws[key] = (arr, ws)
+        return ws
+
+    def _wgrad(self, key, launches, red=None, stream=None):
+        L = _lib.lib()
+        stream = _lib.stream() if stream is None else stream
+        for k, (arr, n) in enumerate(launches):
+            ws = self._wgrad_ws(f'{key}{k}', arr, n)
+            if k == 0 and red is not None:
+                _lib.check(L.drpo_mlp_wgrad_reduce(arr, n, ctypes.byref(red), ws.data_ptr(), ws.numel(), stream),
+                           'ensemble wgrad')
+            else:
+                _lib.check(L.drpo_mlp_wgrad(arr, n, ws.data_ptr(), ws.numel(), stream), 'ensemble wgrad')
 
     def _backward(self, nets, strides, save_x, gD, gL, b, Z):
         L = _lib.lib()
-        d, arr, n = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
+        d, launches = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
         _lib.check(L.drpo_mlp_backward(ctypes.byref(d), _lib.stream()), 'ensemble backward')
-        _lib.check(L.drpo_mlp_wgrad(arr, n, _lib.stream()), 'ensemble wgrad')
+        self._wgrad('cl', launches)
 
     def compute_loss_value(self, s, a, t, with_grads=False, gscale=None):
         """compute_loss on explicit rows (truncated to a multiple of E); returns a 0-d device
@@ -349,7 +372,7 @@ class EnsembleEngine:
         fd, nets, strides, save_x = self._forward_desc(xs, xa, b, Z, b * S, b * A, tag='fit', save=True, z0=z0)
         largs, _, gD, gL = self._loss_args(nets, xs, b * S, xt, b * S1, b, Z, True, loss_out=losses[0:1], tag='fit',
                                            bound=sh is None or sh.rank == 0)
-        bd, warr, nw = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
+        bd, wl = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
         red = EnsReduce()
         full = E * b if sh is not None else rows
         idx_all = None
@@ -387,7 +410,7 @@ class EnsembleEngine:
             # the loss reduction rides as the last workgroup of the wgrad launch
             _lib.check(L.drpo_ens_loss_partials(*largs, ctypes.byref(red), stream), 'ens_loss')
             _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
-            _lib.check(L.drpo_mlp_wgrad_reduce(warr, nw, ctypes.byref(red), stream), 'ensemble wgrad')
+            self._wgrad('fit', wl, red, stream)
             if sh is None:
                 self.dp.sum_(g.grad)
             else:

@@ -63,6 +63,57 @@ class EventTimer:
         return out
 
 
+def _rollout_static(alg, policy, B, H):
+    """The per-(shapes, parameter groups, buffers) part of the rollout descriptor: the
+    packed-mirror and bias pointers, env parameters, normalizer / log-var bound and
+    virtual-buffer pointers, and the workspace. Built once and cached on ``alg``; per
+    call only the members, the noise, the initial-state source and the events change.
+    (Building it took ~20 tensor views per call: most of the call's host time.)"""
+    model = alg.model_ensemble
+    vb = alg.virt_buffer._module
+    pg, mg = policy.group, model.group
+    norm = model.state_normalizer
+    key = (id(policy), B, H, pg.data.data_ptr(), pg.packed.data_ptr(), mg.data.data_ptr(), mg.packed.data_ptr(),
+           norm.mean.data_ptr(), norm.std.data_ptr(), vb._states.data_ptr(), vb.capacity)
+    cache = alg.__dict__.setdefault('_rollout_desc_cache', {})
+    hit = cache.get(key)
+    if hit is not None:
+        return hit
+    L = _lib.lib()
+    S, A, C = alg.state_dim, alg.action_dim, alg.con_dim
+    pa = [(pg.pview(f'net.{2 * i}.weight')[0], pg.view(f'net.{2 * i}.bias')) for i in range(policy.spec.n_layers)]
+
+    def mviews(prefix, spec):   # packed mirrors of member 0 (the kernel adds member * packed size)
+        return [(mg.pview(f'{prefix}{2 * i}.weight')[0], mg.view(f'{prefix}{2 * i}.bias'))
+                for i in range(spec.n_layers)]
+    trunk, diff, logv = (mviews('trunk.', model.trunk_spec), mviews('diff_head.', model.diff_spec),
+                         mviews('log_var_head.', model.logvar_spec))
+    ep = alg.env_params
+    d = RolloutDesc()
+    d.S, d.A, d.C, d.Ha, d.Hm, d.B, d.H = S, A, C, policy.spec.dims[1], model.hidden_dim, B, H
+    d.env_id, d.tracking_surr_start, d.tracking_n_surr = ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr']
+    d.env_thr0, d.env_thr1 = ep['thr0'], ep['thr1']
+    (d.aW1, d.ab1), (d.aW2, d.ab2), (d.aW3, d.ab3) = [(W.data_ptr(), b.data_ptr()) for W, b in pa]
+    (d.mW1, d.mb1), (d.mW2, d.mb2) = [(W.data_ptr(), b.data_ptr()) for W, b in trunk]
+    (d.dW1, d.db1), (d.dW2, d.db2) = [(W.data_ptr(), b.data_ptr()) for W, b in diff]
+    (d.lW1, d.lb1), (d.lW2, d.lb2) = [(W.data_ptr(), b.data_ptr()) for W, b in logv]
+    d.norm_mean, d.norm_std = norm.mean.data_ptr(), norm.std.data_ptr()
+    d.min_lv, d.max_lv = model.min_log_var.data_ptr(), model.max_log_var.data_ptr()
+    d.vs, d.va, d.vs2, d.vr = vb._states.data_ptr(), vb._actions.data_ptr(), vb._next_states.data_ptr(), \
+        vb._rewards.data_ptr()
+    d.vh, d.vd, d.vv = vb._constraint_values.data_ptr(), vb._dones.data_ptr(), vb._violations.data_ptr()
+    d.vptr, d.vcap = vb._pointer.data_ptr(), vb.capacity
+    # a workspace of its own per entry (the cached pointers must never see it reallocated)
+    ws = alg._workspace(f'rollout.{B}.{H}', L.drpo_rollout_workspace_size(B, S, H))
+    d.workspace = ws.data_ptr()
+    members = (ctypes.c_int * H)()
+    d.members = members
+    off = L.drpo_rollout_count_offset(B, S, H)
+    count = ws[off:off + 8].view(torch.int64)[0]
+    hit = cache[key] = (d, members, count)
+    return hit
+
+
 def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
     """One imagined rollout (src/smbpo.py:229-249) into alg.virt_buffer.
 
@@ -74,7 +125,7 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
     L = _lib.lib()
     dev = alg.device
     B, H = alg.rollout_batch_size, alg.horizon
-    S, A, C = alg.state_dim, alg.action_dim, alg.con_dim
+    S, A = alg.state_dim, alg.action_dim
     model = alg.model_ensemble
     rb, vb = alg.replay_buffer._module, alg.virt_buffer._module
     _lib.require_device(policy.group.data, model.group.data, vb._states)
@@ -101,48 +152,21 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
         eps_a_t, eps_m_t = _dev(eps_a, dev), _dev(eps_m, dev)
     else:
         ns = None
-        members = [model._elite_inds[noise.choice(len(model._elite_inds))] for _ in range(H)]
+        elites = model._elite_inds
+        members = [elites[noise.choice(len(elites))] for _ in range(H)]
         eps_a_t = eps_m_t = None
     ctr = noise.next()
 
-    ws = alg._workspace('rollout', L.drpo_rollout_workspace_size(B, S, H))
     start_ptr = vb.pointer if vb._host_ptr is not None else None
     policy.group.ensure_packed()
     model.group.ensure_packed()
-    pa = [(policy.group.pview(f'net.{2 * i}.weight')[0], policy.group.view(f'net.{2 * i}.bias'))
-          for i in range(policy.spec.n_layers)]
-    mg = model.group
-
-    def mviews(prefix, spec):   # packed mirrors of member 0 (the kernel adds member * packed size)
-        return [(mg.pview(f'{prefix}{2 * i}.weight')[0], mg.view(f'{prefix}{2 * i}.bias'))
-                for i in range(spec.n_layers)]
-    actor = pa
-    trunk, diff, logv = (mviews('trunk.', model.trunk_spec), mviews('diff_head.', model.diff_spec),
-                         mviews('log_var_head.', model.logvar_spec))
-    ep = alg.env_params
-    members_arr = (ctypes.c_int * H)(*members)
-    d = RolloutDesc()
-    d.S, d.A, d.C, d.Ha, d.Hm, d.B, d.H = S, A, C, policy.spec.dims[1], model.hidden_dim, B, H
-    d.env_id, d.tracking_surr_start, d.tracking_n_surr = ep['env_id'], ep['tracking_surr_start'], ep['tracking_n_surr']
-    d.env_thr0, d.env_thr1 = ep['thr0'], ep['thr1']
-    (d.aW1, d.ab1), (d.aW2, d.ab2), (d.aW3, d.ab3) = [(W.data_ptr(), b.data_ptr()) for W, b in actor]
-    (d.mW1, d.mb1), (d.mW2, d.mb2) = [(W.data_ptr(), b.data_ptr()) for W, b in trunk]
-    (d.dW1, d.db1), (d.dW2, d.db2) = [(W.data_ptr(), b.data_ptr()) for W, b in diff]
-    (d.lW1, d.lb1), (d.lW2, d.lb2) = [(W.data_ptr(), b.data_ptr()) for W, b in logv]
-    norm = model.state_normalizer
-    d.norm_mean, d.norm_std = norm.mean.data_ptr(), norm.std.data_ptr()
-    d.min_lv, d.max_lv = model.min_log_var.data_ptr(), model.max_log_var.data_ptr()
-    d.members = members_arr
+    d, marr, count = _rollout_static(alg, policy, B, H)
+    marr[:] = members
     d.replay_states, d.replay_ptr, d.replay_cap = src.data_ptr(), src_ptr, src_cap
     d.init_idx = 0 if init_idx is None else init_idx.data_ptr()
     d.eps_a = 0 if eps_a_t is None else eps_a_t.data_ptr()
     d.eps_m = 0 if eps_m_t is None else eps_m_t.data_ptr()
     d.seed, d.ctr = noise.seed, ctr
-    d.vs, d.va, d.vs2, d.vr = vb._states.data_ptr(), vb._actions.data_ptr(), vb._next_states.data_ptr(), \
-        vb._rewards.data_ptr()
-    d.vh, d.vd, d.vv = vb._constraint_values.data_ptr(), vb._dones.data_ptr(), vb._violations.data_ptr()
-    d.vptr, d.vcap = vb._pointer.data_ptr(), vb.capacity
-    d.workspace = ws.data_ptr()
     d.rows_per_tile = getattr(alg, 'rows_per_tile', 0)
     engine = getattr(alg, 'rollout_engine', 0)
     if engine == 0:
@@ -153,8 +177,6 @@ def rollout(alg, policy, initial_states, noise, timer=None, eps_layout=0):
         timer.pairs = 1 if engine == 2 else H   # engine 2: one pair around the fused kernel
     _lib.check(L.drpo_rollout(ctypes.byref(d), _lib.stream()), 'rollout')
     vb._device_advanced()
-    off = L.drpo_rollout_count_offset(B, S, H)
-    count = ws[off:off + 8].view(torch.int64)[0]
     view = _RolloutResult(vb, start_ptr, count)
     view.tape_counts = ns
     return view

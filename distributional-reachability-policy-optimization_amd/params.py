@@ -103,6 +103,17 @@ class FlatGroup:
         cache[key] = dev
         return dev
 
+    def move_grad(self, new_grad, *modules):
+        """Re-home the flat gradient in ``new_grad`` (e.g. a slice of a shared exchange
+        arena), keeping its values; the parameters' .grad views under ``modules`` follow."""
+        assert new_grad.numel() == self.size and new_grad.is_contiguous()
+        new_grad.copy_(self.grad)
+        self.grad = new_grad
+        for mod in modules:
+            for sub in mod.modules():
+                if isinstance(sub, LinearSlot) and sub._group is self:
+                    sub.bind_grad()
+
     def mark_dirty(self):
         """The flat data was written by a kernel (Adam, EMA, a collective)."""
         self._pk_ver = None
@@ -153,11 +164,17 @@ class LinearSlot(nn.Module):
 
     def __init__(self, group, prefix):
         super().__init__()
+        self._group, self._prefix = group, prefix
         self.weight = nn.Parameter(group.view(prefix + 'weight'), requires_grad=False)
         self.bias = nn.Parameter(group.view(prefix + 'bias'), requires_grad=False)
-        if group.grad is not None:          # target groups (frozen) carry no gradient storage
-            self.weight.grad = group.view(prefix + 'weight', group.grad)
-            self.bias.grad = group.view(prefix + 'bias', group.grad)
+        self.bind_grad()
+
+    def bind_grad(self):
+        """.grad views into the group's flat gradient (again after it moved)."""
+        g, p = self._group, self._prefix
+        if g.grad is not None:              # target groups (frozen) carry no gradient storage
+            self.weight.grad = g.view(p + 'weight', g.grad)
+            self.bias.grad = g.view(p + 'bias', g.grad)
 
 
 class Squeeze(nn.Module):

@@ -94,10 +94,16 @@ def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, ws
     return d
 
 
-def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None, split_heads=False):
+UPSTREAM_GOUT, UPSTREAM_CRITIC, UPSTREAM_CERT = 0, 1, 2   # drpo_mlp_bwd_t.upstream
+
+
+def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None, split_heads=False, upstream=0):
     """nets[0] trunk when trunk=True (gouts[0] ignored); dx: {net_index: (tensor, col0, cols, accumulate)};
-    split_heads: one workgroup per head, the second head's trunk dZ share into nets[0].dz2."""
+    split_heads: one workgroup per head, the second head's trunk dZ share into nets[0].dz2;
+    upstream: output gradients from the gout arrays, or formed in-kernel from the
+    launch's critic head (UPSTREAM_CRITIC / UPSTREAM_CERT)."""
     d = MlpBwd()
+    d.upstream = upstream
     for j, net in enumerate(nets):
         d.net[j].nl = len(net.layers)
         for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
@@ -127,18 +133,39 @@ def with_head(d, mode, A, eps, site, a=None, logp=None, u=None, e=None, amean=No
     return d
 
 
-def wgrad_items(entries, rows):
-    """entries: [(net, inputs_per_layer)] -> ctypes array of WgradItem."""
-    items = []
-    for net, ins in entries:
+def wgrad_items(entries, rows, sq=None):
+    """entries: [(net, inputs_per_layer[, segment])] -> (ctypes array of WgradItem, count,
+    {segment: partial slots used}). With sq = {segment: device tensor}, every item of a
+    segment writes the sums of squares of its finished gradient tiles into consecutive
+    slots of that segment's tensor (the clip partials of drpo_optim_step)."""
+    L = _lib.lib()
+    items, used = [], {}
+    for ent in entries:
+        net, ins = ent[0], ent[1]
+        seg = ent[2] if len(ent) > 2 else None
         for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
             gW, gb = net.grad_layers[l]
             it = WgradItem()
             it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
             it.dout, it.din, it.rows, it.nbatch = dout, din, rows, 1
+            if sq is not None and seg is not None:
+                it.sq, it.sq_off = sq[seg].data_ptr(), used.get(seg, 0)
+                used[seg] = it.sq_off + L.drpo_mlp_wgrad_tiles(ctypes.byref(it))
+                assert used[seg] <= sq[seg].numel(), 'clip partial buffer too small'
             items.append(it)
     arr = (WgradItem * len(items))(*items)
-    return arr, len(items)
+    return arr, len(items), used
+
+
+def wgrad_workspace(cache, key, arr, n, dev):
+    """Zero-initialised workspace of one drpo_mlp_wgrad call site (the launches keep it
+    zeroed), cached by key and grown when the plan needs more."""
+    need = int(_lib.lib().drpo_mlp_wgrad_workspace_size(arr, n))
+    t = cache.get(key)
+    if t is None or t.numel() < need:
+        t = torch.zeros(max(need, 256), dtype=torch.uint8, device=dev)
+        cache[key] = t
+    return t
 
 
 def fwd_flops(d):
@@ -164,6 +191,7 @@ def bwd_flops(d):
 
 
 def wgrad_flops(arr, n):
+    # (arr, n[, used]) descriptors
     return sum(2 * arr[i].rows * arr[i].nbatch * arr[i].dout * (arr[i].din + 1) for i in range(n))
 
 
@@ -212,6 +240,17 @@ class SACEngine:
             not solver.distributional_qc else None
         self.B = None
         self.ws = {}
+        self.wg_ws = {}
+        # The actor update's data-parallel exchange is ONE all-reduce:
+        # the actor's and the safe actor's flat gradients and the alpha-loss sum are
+        # adjacent slices of one arena (the critic and multiplier phases already exchange
+        # one flat buffer each).
+        ga, gs = solver.actor.group, solver.actor_safe.group
+        na, ns = ga.size, gs.size
+        self.actor_xchg = torch.zeros(na + ns + 64, device=self.dev)
+        ga.move_grad(self.actor_xchg[:na], solver.actor)
+        gs.move_grad(self.actor_xchg[na:na + ns], solver.actor_safe)
+        self.alpha_sum = self.actor_xchg[na + ns:na + ns + 1]   # zeroed by the step that consumes it
         self.loss_pool = None
         self.loss_pos = 0
         self._zeroed = set()   # groups whose grads the last fused step left zeroed
@@ -332,7 +371,7 @@ class SACEngine:
         if ev:
             self.profiler.end(ev)
 
-    def _run_bwd_multi(self, key, builder):
+    def _run_bwd_multi(self, key, builder, head=None):
         d = self.desc.get(key)
         if d is None:
             jobs = builder()
@@ -340,7 +379,11 @@ class SACEngine:
             d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(bwd_flops(j) for j in jobs))
         arr, dev, nj, fl = d
         ev = self.profiler.begin('mlp_bwd', key, fl) if self.profiler else None
-        _lib.check(_lib.lib().drpo_mlp_backward_multi(arr, dev.data_ptr(), nj, _lib.stream()), key)
+        if head is None:
+            _lib.check(_lib.lib().drpo_mlp_backward_multi(arr, dev.data_ptr(), nj, _lib.stream()), key)
+        else:
+            _lib.check(_lib.lib().drpo_mlp_backward_multi_head(arr, dev.data_ptr(), nj, ctypes.byref(head),
+                                                               _lib.stream()), key)
         if ev:
             self.profiler.end(ev)
 
@@ -354,14 +397,36 @@ class SACEngine:
             self.profiler.end(ev)
 
     def _run_wgrad(self, key, builder):
+        """One grouped weight-gradient launch; returns the clip-partial slots per segment."""
         d = self.desc.get(key)
         if d is None:
-            d = self.desc[key] = builder()
-        arr, n = d
+            arr, n, used = builder()
+            ws = wgrad_workspace(self.wg_ws, key, arr, n, self.dev)
+            d = self.desc[key] = (arr, n, used, ws)
+        arr, n, used, ws = d
         ev = self.profiler.begin('mlp_wgrad', key, wgrad_flops(arr, n)) if self.profiler else None
-        _lib.check(_lib.lib().drpo_mlp_wgrad(arr, n, _lib.stream()), key)
+        _lib.check(_lib.lib().drpo_mlp_wgrad(arr, n, ws.data_ptr(), ws.numel(), _lib.stream()), key)
         if ev:
             self.profiler.end(ev)
+        return used
+
+    def _clip_parts(self, fused, key, segs, grads):
+        """Clip partial sums per segment: from the weight-gradient launch (fused, single
+        process) or, after a data-parallel all-reduce, one sum-of-squares launch over
+        the reduced gradient slices."""
+        if fused is not None:
+            return [self.buf(f'sq.{key}.{sg}', 4096)[:fused[sg]] for sg in segs]
+        L = _lib.lib()
+        parts = [self.buf(f'part.{key}.{sg}', 4096)[:L.drpo_grad_sumsq_blocks(g.numel())] for sg, g in zip(segs, grads)]
+        grad_sumsq_multi(grads, parts)
+        return parts
+
+    def _sq(self, key, segs):
+        """{segment: partial buffer} for a fused-clip weight-gradient launch, or None
+        under data parallelism (the norm must be of the all-reduced gradient)."""
+        if self.dp.active:
+            return None
+        return {sg: self.buf(f'sq.{key}.{sg}', 4096) for sg in segs}
 
     def _policy_head(self, raw, mode, eps, site, ctr, a=None, logp=None, u=None, e=None, amean=None):
         L = _lib.lib()
@@ -482,29 +547,30 @@ class SACEngine:
         ch.dc = ws['c.dm'].data_ptr() if robust else 0
         ch.seed, ch.ctr = noise.seed, ctr
         ch.loss = loss.data_ptr()
-        _lib.check(L.drpo_critic_head(ctypes.byref(ch), _lib.stream()), 'critic_head')
-        # backward: critics (twin) and constraint critic (trunk + heads)
+        # backward: critics (twin) and constraint critic (trunk + heads), each job forming
+        # its own output gradients (and loss) from the critic head in-kernel
+        # (src/ssac.py:284-456: compute_target, compute_cons_target, both losses)
         heads = [n['cc_trunk'], n['cc_mean']] + ([n['cc_ls']] if dist else [])
         self._run_bwd_multi('c.b' + str(int(dist)), lambda: [
-            fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)], B, trunk=True),
-            fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B)])
+            fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)], B, trunk=True, upstream=UPSTREAM_CERT),
+            fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B, upstream=UPSTREAM_CRITIC)], head=ch)
         tsy = n['cc_trunk'].sy
-        items = [(n['q0'], [xs, n['q0'].sy[0], n['q0'].sy[1]]), (n['q1'], [xs, n['q1'].sy[0], n['q1'].sy[1]]),
-                 (n['cc_trunk'], [xs, tsy[0]]), (n['cc_mean'], [tsy[-1], n['cc_mean'].sy[0]])]
+        items = [(n['q0'], [xs, n['q0'].sy[0], n['q0'].sy[1]], 'c'), (n['q1'], [xs, n['q1'].sy[0], n['q1'].sy[1]], 'c'),
+                 (n['cc_trunk'], [xs, tsy[0]], 'cc'), (n['cc_mean'], [tsy[-1], n['cc_mean'].sy[0]], 'cc')]
         if dist:
-            items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]]))
-        self._run_wgrad('c.wg' + str(int(dist)), lambda: wgrad_items(items, B))
+            items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]], 'cc'))
+        sq = self._sq('c', ('c', 'cc'))
+        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq))
         cg = sol.critic_group
         self.dp.sum_(cg.grad)      # the 1/G of the mean rides in the optimizer segments
         crange = cg.span('critic.')
         ccrange = self._alive_span(cg, ['constraint_critic.trunk.', 'constraint_critic.mean_head.'] +
                                    (['constraint_critic.log_std_head.'] if dist else []))
         # two clip norms (critic, constraint critic), one Adam step, grad zeroing, EMA of
-        # the whole target group and the packed-mirror refresh: 2 launches
+        # the whole target group and the packed-mirror refresh: one launch
         tg = sol.critic_target_group
-        parts = [self.buf(f'part.c.{s0}', 4096)[:_lib.lib().drpo_grad_sumsq_blocks(s1 - s0)] for s0, s1 in
-                 (crange, ccrange)]
-        grad_sumsq_multi([cg.grad[s0:s1] for s0, s1 in (crange, ccrange)], parts)
+        parts = self._clip_parts(used if sq else None, 'c', ('c', 'cc'),
+                                 [cg.grad[s0:s1] for s0, s1 in (crange, ccrange)])
         sc = sol.critic_optimizer.step_scalars()
         mp = cg.pack_map(tg)
         segs = [sol.critic_optimizer.segment(s0, s1, sc, clip=(pt, sol.grad_norm), zero_grad=True,
@@ -605,12 +671,13 @@ class SACEngine:
             fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B, trunk=True,
                      dx={0: (dAs, S, A, False)}),
             fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)})])
-        # squashed Gaussian backward -> actor heads; alpha loss sum
-        asum = self._loss_slots(1)
+        # squashed Gaussian backward -> actor heads; alpha loss sum (exchange-arena slot)
+        asum = self.alpha_sum
         draw, draws = self.buf('a.draw', B, 2 * A), self.buf('a.draws', B, 2 * A)
         _lib.check(L.drpo_squash_backward(B, A, raw.data_ptr(), u.data_ptr(), e.data_ptr(), dA.data_ptr(),
                                           dAc.data_ptr(), sol.log_alpha.data_ptr(), 1.0 / B, lp.data_ptr(),
-                                          float(sol.target_entropy), asum.data_ptr(), draw.data_ptr(),
+                                          float(sol.target_entropy), asum.data_ptr() if sol.autotune_alpha else None,
+                                          draw.data_ptr(),
                                           _lib.stream()), 'squash_backward')
         _lib.check(L.drpo_squash_backward(B, A, raws.data_ptr(), u_s.data_ptr(), e_s.data_ptr(), dAs.data_ptr(),
                                           None, None, 0.0, None, 0.0, None, draws.data_ptr(), _lib.stream()),
@@ -619,22 +686,20 @@ class SACEngine:
         self._clean_grads(sol.actor_safe.group)
         self._run_bwd_multi('a.bpi', lambda: [fill_bwd([n['actor']], [draw], B), fill_bwd([n['safe']], [draws], B)])
         na, ns = n['actor'], n['safe']
-        self._run_wgrad('a.wg', lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]]), (ns, [xs, ns.sy[0], ns.sy[1]])],
-                                                    B))
+        sq = self._sq('a', ('a', 's'))
+        used = self._run_wgrad('a.wg' + ('f' if sq else ''),
+                               lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]], 'a'),
+                                                    (ns, [xs, ns.sy[0], ns.sy[1]], 's')], B, sq))
         # d alpha_loss / d log_alpha = -exp(log_alpha) * mean(logp + target_entropy) is formed
         # inside the optimizer launch from the alpha-loss sum (src/ssac.py:498-501); under
         # DP the sum is sum-reduced and divided by G*B rows (same value: log_alpha is
         # replicated). The actors' 1/G rides in their optimizer segments.
-        ag = self.buf('a.alpha_grad', 1)
-        self.dp.sum_(sol.actor.group.grad, sol.actor_safe.group.grad, asum)
+        self.dp.sum_(self.actor_xchg)        # actor + safe actor grads + alpha-loss sum: one bucket
         gsc = self.dp.scale
         # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam +
-        # cosine -- one sum-of-squares launch and one fused optimizer launch
+        # cosine -- one fused optimizer launch (clip partials from the weight gradients)
         ga, gs = sol.actor.group, sol.actor_safe.group
-        L = _lib.lib()
-        pa = self.buf('part.a', 4096)[:L.drpo_grad_sumsq_blocks(ga.size)]
-        ps = self.buf('part.s', 4096)[:L.drpo_grad_sumsq_blocks(gs.size)]
-        grad_sumsq_multi([ga.grad, gs.grad], [pa, ps])
+        pa, ps = self._clip_parts(used if sq else None, 'a', ('a', 's'), [ga.grad, gs.grad])
         aopt = sol.alpha_optimizer
         if aopt.tensor is None:
             aopt.tensor = sol.log_alpha.view(1)
@@ -644,8 +709,9 @@ class SACEngine:
         # its "i == 2" clip / schedule of the safe actor never fires (src/ssac.py:507-527)
         safe_full = sol.autotune_alpha
         if sol.autotune_alpha:
-            segs.append(aopt.segment(0, 1, aopt.step_scalars(), grad=ag, grad_from_sum=(asum, B * self.dp.world),
-                                     grad_from_sum_kind=2 if sol.use_log_alpha_loss else 0))
+            # the gradient is formed from the sum; zero_grad clears the sum slot for the next step
+            segs.append(aopt.segment(0, 1, aopt.step_scalars(), grad=asum, grad_from_sum=(asum, B * self.dp.world),
+                                     grad_from_sum_kind=2 if sol.use_log_alpha_loss else 0, zero_grad=True))
         segs.append(sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
                                                      clip=(ps, sol.grad_norm) if safe_full else None, zero_grad=True,
                                                      pack_map=gs.pack_map(), grad_scale=gsc))
@@ -739,10 +805,11 @@ class SACEngine:
         self._clean_grads(g)
         nm = n['mult']
         self._run_bwd('m.bmult', lambda: fill_bwd([nm], [gx], B))
-        self._run_wgrad('m.wg', lambda: wgrad_items([(nm, [xm, nm.sy[0], nm.sy[1]])], B))
+        sq = self._sq('m', ('m',))
+        used = self._run_wgrad('m.wg' + ('f' if sq else ''),
+                               lambda: wgrad_items([(nm, [xm, nm.sy[0], nm.sy[1]], 'm')], B, sq))
         self.dp.sum_(g.grad)
-        pm = self.buf('part.m', 4096)[:_lib.lib().drpo_grad_sumsq_blocks(g.size)]
-        grad_sumsq_multi([g.grad], [pm])
+        pm, = self._clip_parts(used if sq else None, 'm', ('m',), [g.grad])
         fused_step([sol.multiplier_optimizer.segment(0, g.size, sol.multiplier_optimizer.step_scalars(),
                                                      clip=(pm, sol.grad_norm), zero_grad=True,
                                                      pack_map=g.pack_map(), grad_scale=self.dp.scale)])

@@ -172,7 +172,7 @@ typedef struct {
   float* dz;           /* optional save of dL/dZ for weight gradients */
   int64_t wstride;
   float* dz2;          /* split_heads trunk layers: the second head's partial dL/dZ (trunk
-                          dZ = dz + dz2: one wgrad item per term, both accumulate into dW) */
+                          dZ = dz + dz2) */
 } drpo_mlp_bwd_layer_t;
 
 typedef struct {
@@ -192,17 +192,29 @@ typedef struct {
   int split_heads;     /* trunk mode, single launches, trunk dx unused: one workgroup per (row
                           tile, head) backs its head's gradient through the trunk (linear in
                           the head gradients), writing dz (head 1) / dz2 (head 2) */
+  int upstream;        /* where the output gradients come from: DRPO_UPSTREAM_* */
 } drpo_mlp_bwd_t;
+
+/* drpo_mlp_bwd_t.upstream */
+#define DRPO_UPSTREAM_GOUT 0     /* the nets' gout arrays */
+#define DRPO_UPSTREAM_CRITIC 1   /* twin-critic job: net k's output gradient is (q_k - y) / B with the soft
+                                    Bellman target y of the launch's critic head; adds the critic loss */
+#define DRPO_UPSTREAM_CERT 2     /* constraint-critic job (trunk + mean [+ log-std] heads): the
+                                    certificate loss gradients of the launch's critic head; adds its loss */
 
 typedef struct {
   const float* dz; /* [rows][dout] */
   const float* y;  /* layer input [rows][din] */
-  float* gW;       /* accumulated into (atomics): caller zeroes before the backward pass */
-  float* gb;
+  float* gW;       /* gW += dZ^T Y (no two items of one launch may share gW) */
+  float* gb;       /* gb += colsum(dZ) */
   int dout, din;
   int64_t rows;
   int64_t zstride, ystride, gwstride, gbstride;
   int nbatch;
+  float* sq;       /* optional clip partials: sq[sq_off + t] = sum of squares of the
+                      FINISHED gradient (weights + bias) of output tile t of this item,
+                      t < drpo_mlp_wgrad_tiles(item) (summed by drpo_optim_step) */
+  int sq_off;
 } drpo_wgrad_item_t;
 
 /* the reduction step of drpo_ens_loss, as data: run by drpo_mlp_wgrad_reduce */
@@ -215,6 +227,27 @@ typedef struct {
   float *mse, *loss, *gmin, *gmax;
 } drpo_ens_reduce_t;
 
+/* the safe-SAC critic losses of one update_critic (src/ssac.py:284-435): drpo_critic_head
+ * (csrc/sac.hip) or fused into drpo_mlp_backward_multi_head */
+typedef struct {
+  int64_t B;
+  int C;
+  int distributional, deterministic_backup;
+  float discount, qc_td_bound, lmin, lmax;
+  const float* log_alpha;
+  const float *r, *h;
+  const uint8_t* d;
+  const uint8_t* dc;    /* certificate-target done flags (robust branch: model-predicted); NULL = d */
+  const float *q0t, *q1t, *logp2;
+  const float *mu_t, *ls_t;
+  const float* eps3;
+  uint64_t seed, ctr;
+  const float *q0, *q1;
+  const float *mu, *ls;
+  float *dq0, *dq1, *dmu, *dls;
+  float* loss; /* [2] accumulated: critic loss, constraint-critic loss */
+} drpo_critic_head_t;
+
 int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);
 /* Up to 8 independent forward jobs (different inputs / nets, e.g. every forward of
  * one SAC loss that does not depend on another) in ONE launch, each with an
@@ -226,11 +259,27 @@ int drpo_mlp_backward(const drpo_mlp_bwd_t* desc /* host */, drpo_stream_t strea
 /* independent backward-data jobs in one launch (descriptors in device memory) */
 int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
                             drpo_stream_t stream);
-int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, drpo_stream_t stream);
+/* the same with the critic losses fused in (update_critic, src/ssac.py:284-456): jobs with
+ * upstream = DRPO_UPSTREAM_CRITIC / _CERT form their output gradients from `head` (the
+ * forward outputs, targets and batch of drpo_critic_head_t; its dq0 / dq1 / dmu / dls are
+ * not written, loss[0] / loss[1] are accumulated) -- no separate head launch */
+int drpo_mlp_backward_multi_head(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                                 const drpo_critic_head_t* head /* host */, drpo_stream_t stream);
+/* Weight gradients of up to 16 layers (items) in ONE launch: gW += dZ^T Y, gb +=
+ * colsum(dZ) (the autograd of nn.Linear / BatchedLinear, src/dynamics.py:26-52,
+ * src/torch_util.py:190-211), split into (output tile x row chunk) workgroups whose
+ * partial tiles are combined in a fixed order by the tile's last workgroup (no float
+ * atomics: deterministic). workspace: drpo_mlp_wgrad_workspace_size(items, n) bytes,
+ * ZEROED by the caller once before its first use (the launch leaves it zeroed). */
+size_t drpo_mlp_wgrad_workspace_size(const drpo_wgrad_item_t* items /* host */, int n);
+/* output tiles of one item (the number of sq partials it writes) */
+int drpo_mlp_wgrad_tiles(const drpo_wgrad_item_t* item /* host */);
+int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, void* workspace, size_t workspace_bytes,
+                   drpo_stream_t stream);
 /* drpo_mlp_wgrad plus one extra workgroup running a deferred ensemble-loss
  * reduction (drpo_ens_loss_partials); red may be NULL */
 int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items /* host */, int n, const drpo_ens_reduce_t* red /* host */,
-                          drpo_stream_t stream);
+                          void* workspace, size_t workspace_bytes, drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- packed weight mirrors
  * Every MLP kernel streams weights from fragment-linear mirrors of the PyTorch
@@ -279,24 +328,6 @@ int drpo_cc_dist(const float* mu, const float* lsraw, int64_t n, int mode, float
 int drpo_cc_head(const float* mu, const float* lsraw, int64_t B, int C, int distributional, float std_ratio,
                  float log_std_min, float log_std_max, float* ubmax, int* argmax, drpo_stream_t stream);
 
-typedef struct {
-  int64_t B;
-  int C;
-  int distributional, deterministic_backup;
-  float discount, qc_td_bound, lmin, lmax;
-  const float* log_alpha;
-  const float *r, *h;
-  const uint8_t* d;
-  const uint8_t* dc;    /* certificate-target done flags (robust branch: model-predicted); NULL = d */
-  const float *q0t, *q1t, *logp2;
-  const float *mu_t, *ls_t;
-  const float* eps3;
-  uint64_t seed, ctr;
-  const float *q0, *q1;
-  const float *mu, *ls;
-  float *dq0, *dq1, *dmu, *dls;
-  float* loss; /* [2] accumulated: critic loss, constraint-critic loss */
-} drpo_critic_head_t;
 
 /* compute_target + compute_cons_target + critic / constraint-critic losses and
  * their output gradients (src/ssac.py:284-435) */

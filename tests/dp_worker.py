@@ -58,16 +58,28 @@ def main():
         t = drpo_amd.TapeNoise.from_npz(d, name)
         return drpo_amd.TapeNoise(shard_tape(t.entries, B, rank, world))
 
+    from drpo_amd.distributed import CommLog
+
+    def one_bucket(phase, c0):   # each update exchanges ONE all-reduce bucket
+        n = CommLog.calls - c0
+        assert n == 1, f'rank {rank}: {phase} issued {n} collectives'
+
+    c0 = CommLog.calls
     sol.update_critic(*batch, noise=tape('critic_tape'))
     torch.cuda.synchronize()
+    one_bucket('update_critic', c0)
     check_params(sol, solver_sd(d, 'sd1/'), f'rank {rank} after update_critic')
+    c0 = CommLog.calls
     sol.update_actor_and_alpha(batch[0], noise=tape('actor_tape'))
     torch.cuda.synchronize()
+    one_bucket('update_actor_and_alpha', c0)
     ref2 = solver_sd(d, 'sd2/')
     np.testing.assert_allclose(sol.log_alpha.item(), float(ref2['log_alpha']), rtol=1e-5, atol=1e-6)
     check_params(sol, ref2, f'rank {rank} after update_actor_and_alpha')
+    c0 = CommLog.calls
     sol.update_multiplier(batch[0], noise=tape('mult_tape'))
     torch.cuda.synchronize()
+    one_bucket('update_multiplier', c0)
     check_params(sol, solver_sd(d, 'sd3/'), f'rank {rank} after update_multiplier')
     dist.barrier()
     dist.destroy_process_group()

@@ -78,3 +78,26 @@ def test_buffer_circular_host_semantics():
     r = buf.get('rewards')
     assert r.tolist() == [100., 101., 102., 103., 2.][-5:] or r.tolist() == [2., 100., 101., 102., 103.]
     assert r.tolist() == [2., 100., 101., 102., 103.]
+
+
+def test_actor_exchange_arena_rehomes_parameter_grads():
+    """The actor update's single data-parallel bucket: the actor's and
+    the safe actor's flat gradients moved into adjacent slices of one arena keep their
+    values, and every nn.Parameter's .grad follows into the arena."""
+    alg = make_smbpo('quadrotor')
+    sol = alg.solver
+    ga, gs = sol.actor.group, sol.actor_safe.group
+    ga.grad.normal_()
+    gs.grad.normal_()
+    va, vs = ga.grad.clone(), gs.grad.clone()
+    arena = torch.zeros(ga.size + gs.size + 64)
+    ga.move_grad(arena[:ga.size], sol.actor)
+    gs.move_grad(arena[ga.size:ga.size + gs.size], sol.actor_safe)
+    assert torch.equal(arena[:ga.size], va) and torch.equal(arena[ga.size:ga.size + gs.size], vs)
+    base, end = arena.data_ptr(), arena.data_ptr() + 4 * arena.numel()
+    for mod in (sol.actor, sol.actor_safe):
+        for name, p in mod.named_parameters():
+            assert p.grad is not None and base <= p.grad.data_ptr() < end, name
+    w = sol.actor.net[0].weight
+    w.grad.add_(1.0)                      # a write through a parameter's .grad lands in the arena
+    assert torch.equal(arena[ga.offset('net.0.weight')], va[ga.offset('net.0.weight')] + 1.0)
