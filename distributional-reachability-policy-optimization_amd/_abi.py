@@ -58,6 +58,12 @@ class EnsReduce(ctypes.Structure):
                 ('weight', c_float), ('gscale', P), ('mse', P), ('loss', P), ('gmin', P), ('gmax', P)]
 
 
+class EnsUpstream(ctypes.Structure):
+    """drpo_ens_upstream_t"""
+    _fields_ = [('D', P), ('LVR', P), ('s', P), ('s_zstride', c_int64), ('t', P), ('t_zstride', c_int64),
+                ('b', c_int64), ('S', c_int), ('Z', c_int), ('minlv', P), ('maxlv', P), ('gscale', P), ('part', P)]
+
+
 # name -> (restype, argtypes)
 PROTOTYPES = {
     'drpo_version': (c_int, []),
@@ -177,6 +183,8 @@ PROTOTYPES.update({
     'drpo_mlp_backward_multi_head': (c_int, [POINTER(MlpBwd), P, c_int, POINTER(CriticHead), P]),
     'drpo_mlp_backward_multi': (c_int, [POINTER(MlpBwd), P, c_int, P]),
     'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
+    'drpo_mlp_backward_ens': (c_int, [POINTER(MlpBwd), POINTER(EnsUpstream), POINTER(EnsReduce), POINTER(EnsReduce),
+                                      P]),
     'drpo_mlp_wgrad_workspace_size': (c_size_t, [POINTER(WgradItem), c_int]),
     'drpo_mlp_wgrad_tiles': (c_int, [POINTER(WgradItem)]),
     'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P, c_size_t, P]),

@@ -139,6 +139,9 @@ def build(verbose=False, jobs=8, variant=None, defines=(), tag=None):
     into libdrpo_hip_stamps.so; never loaded by the product. ``defines`` + ``tag``: an
     A/B build with extra -D macros into libdrpo_hip[_stamps]_<tag>.so (loaded only via
     DRPO_LIB_OVERRIDE by the profiling scripts)."""
+    if defines and not tag:
+        # an A/B build must never overwrite the production library (nor silently drop its -D's)
+        raise ValueError('build(defines=...) needs a tag: the variant goes to libdrpo_hip[_stamps]_<tag>.so')
     flags = FLAGS + ['-D' + d for d in defines]
     suffix = f'_{tag}' if tag else ''
     if variant == 'stamps':

@@ -277,16 +277,21 @@ struct GSave {
 // bias values of this lane's output columns, loaded before the k-loop so their
 // latency hides behind it (loaded after the loop they cost a full L2 round trip
 // per layer)
+// (The rollout's DRPO_ABIAS_LDS A/B build stages the actor biases in LDS; only that
+// build carries the address-space test, so default builds keep one plain global load.)
 template <int NW, int MAXC>
 __device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N, float (&bv)[MAXC]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int col = (wave + NW * c) * 16 + (lane & 15);
-    if (bias && __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)bias))   // LDS-staged
+#if defined(DRPO_ABIAS_LDS) && DRPO_ABIAS_LDS
+    if (bias && __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)bias)) {   // LDS-staged
       bv[c] = col < N ? ((const __attribute__((address_space(3))) float*)(bias))[col] : 0.f;
-    else
-      bv[c] = (bias && col < N) ? gload(bias + col) : 0.f;
+      continue;
+    }
+#endif
+    bv[c] = (bias && col < N) ? gload(bias + col) : 0.f;
   }
 }
 

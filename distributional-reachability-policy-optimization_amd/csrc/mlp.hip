@@ -578,9 +578,84 @@ __device__ __forceinline__ void cert_upstream(CriticHeadK& ch, const drpo_mlp_bw
   wave_loss_add(lc, ch.loss + 1);
 }
 
+// the fit's upstream, read in place from the kernarg segment (see CriticHeadK)
+typedef const __attribute__((address_space(4))) drpo_ens_upstream_t EnsUpK;
+
+// DRPO_UPSTREAM_ENS: the heteroscedastic NLL of rows [row0, row0+nrows) of member z
+// (drpo_ens_loss's arithmetic, csrc/ensemble.hip; src/dynamics.py:143-153,236-253):
+// d loss / d diff-head -> Gd, d loss / d raw log-var -> Gl (+ the output layers' saved
+// dZ), and this tile's loss partials (mse, and per column the min / max log-var bound
+// gradients) at partial block (z, bx) of the drpo_ens_loss workspace layout. Cm / Cx:
+// LDS scratch (16 rows each). Thread t owns column t % 16-padded-width of row t / width,
+// the element mapping and summation order of ens_loss_kernel at S+1 <= 16.
+__device__ __forceinline__ void ens_upstream(EnsUpK& u, const drpo_mlp_bwd_net_t& hd, const drpo_mlp_bwd_net_t& hl,
+                                             float* Gd, float* Gl, float* Cm, float* Cx, int z, int bx, int row0,
+                                             int nrows) {
+  const int tid = threadIdx.x;
+  const int S = u.S, S1 = S + 1, opad = round_up(S1, 16);
+  const int64_t b = u.b;
+  const float inv_n = 1.f / (float)(b * S1);
+  const float g = (u.gscale ? *u.gscale : 1.f) * inv_n;
+  float acc = 0.f;
+  for (int e = tid; e < FW_ROWS * opad; e += FW_NT) {
+    const int r = e / opad, k = e - r * opad;
+    float gd = 0.f, gl = 0.f, cmn = 0.f, cmx = 0.f;
+    if (r < nrows && k < S1) {
+      const int64_t row = row0 + r;
+      const int64_t o = ((int64_t)z * b + row) * S1 + k;
+      const float hi = u.maxlv[k], lo = u.minlv[k];
+      const float raw = u.LVR[o];
+      const float l1 = hi - softplusf(hi - raw);
+      const float l = lo + softplusf(l1 - lo);
+      const float m = u.D[o] + (k < S ? u.s[(int64_t)z * u.s_zstride + row * S + k] : 0.f);
+      const float diff = u.t[(int64_t)z * u.t_zstride + row * S1 + k] - m;
+      const float iv = expf(-l);
+      acc += diff * diff * iv + l;
+      const float dl = (1.f - diff * diff * iv) * g;
+      const float s1 = sp_grad(l1 - lo), s2 = sp_grad(hi - raw);
+      gd = -2.f * diff * iv * g;
+      gl = dl * s1 * s2;
+      cmn = dl * (1.f - s1);
+      cmx = dl * s1 * (1.f - s2);
+      if (hd.L[1].dz) gstore(hd.L[1].dz + o, gd);
+      if (hl.L[1].dz) gstore(hl.L[1].dz + o, gl);
+    }
+    Gd[r * LDH + k] = gd;
+    Gl[r * LDH + k] = gl;
+    Cm[r * LDH + k] = cmn;
+    Cx[r * LDH + k] = cmx;
+  }
+  // mse partial: per-wave sums, then the waves in order (thread 0)
+  float v = acc * inv_n;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  __shared__ float s_red[FW_NW];
+  if ((tid & 63) == 0) s_red[tid >> 6] = v;
+  lds_barrier();
+  const int nbx = (int)((b + FW_ROWS - 1) / FW_ROWS);
+  float* part_mse = u.part;
+  float* part_min = part_mse + (size_t)u.Z * nbx;
+  float* part_max = part_min + (size_t)u.Z * nbx * S1;
+  const size_t pb = (size_t)z * nbx + bx;
+  if (tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < FW_NW; ++w) t += s_red[w];
+    part_mse[pb] = t;
+  }
+  if (tid < S1) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int r = 0; r < FW_ROWS; ++r) {
+      a0 += Cm[r * LDH + tid];
+      a1 += Cx[r * LDH + tid];
+    }
+    part_min[pb * S1 + tid] = a0;
+    part_max[pb * S1 + tid] = a1;
+  }
+}
+
 // heads' output gradients -> trunk-output gradient in G (bA, bB, DT are scratch)
 __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restrict__ a, float* G, float* bA, float* bB,
-                                                 float* DT, int z, int row0, int nrows, CriticHeadK* ch) {
+                                                 float* DT, int z, int row0, int nrows, CriticHeadK* ch,
+                                                 EnsUpK* eu = nullptr) {
   const int tid = threadIdx.x;
   const drpo_mlp_bwd_net_t &h1 = a.net[1], &h2 = a.net[2];
   const int hid = h1.L[0].dout, out = h1.L[1].dout;
@@ -589,7 +664,8 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
   bwd_fetch_act(h1.L[0], z, a.rows, row0, nrows, sv1);   // head 1's hidden saved values, one phase ahead
   // output layers (identity): dZ = the given output gradient, saved for the weight gradients
   const size_t so = ((size_t)z * a.rows + row0) * out;
-  if (ch) cert_upstream(*ch, h1, &h2, G, bA, row0, nrows);
+  if (eu) ens_upstream(*eu, h1, h2, G, bA, bB, DT, z, row0 / FW_ROWS, row0, nrows);
+  else if (ch) cert_upstream(*ch, h1, &h2, G, bA, row0, nrows);
   else
   for (int e = tid; e < 2 * FW_ROWS * opad; e += FW_NT) {
     const int w = e / (FW_ROWS * opad), e2 = e - w * FW_ROWS * opad;
@@ -644,7 +720,7 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
 // one (job, net) slot of the fused backward-data pass; `a` may live in kernarg
 // (single launch) or global memory (multi-job launch)
 __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, int sel, int bx, int bz, float* smem,
-                                         CriticHeadK* ch = nullptr) {
+                                         CriticHeadK* ch = nullptr, EnsUpK* eu = nullptr) {
   float* G = smem;
   float* bA = G + FW_ROWS * LDH;
   float* bB = bA + FW_ROWS * LDH;
@@ -715,7 +791,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     return;
   }
   if (bwd_paired_heads(a)) {
-    bwd_heads_paired(a, G, bA, bB, DT, z, row0, nrows, hc);
+    bwd_heads_paired(a, G, bA, bB, DT, z, row0, nrows, hc, a.upstream == DRPO_UPSTREAM_ENS ? eu : nullptr);
     const float* gx = bwd_net(a.net[0], G, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
     if (gx) store_dx(a.net[0], gx);
     return;
@@ -752,6 +828,21 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const LogicalBlock lb = xcd_block();   // one member's tiles per XCD (shared weights in L2)
   bwd_body(a, lb.y, lb.x, lb.z, smem);
+}
+
+// the model fit's backward with the NLL loss fused in (one workgroup per (row tile,
+// member); drpo_mlp_backward_ens)
+struct BwdEnsArgs {
+  drpo_mlp_bwd_t a;
+  drpo_ens_upstream_t u;
+};
+
+__global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_ens_kernel(BwdEnsArgs m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  typedef const __attribute__((address_space(4))) BwdEnsArgs* ArgsK;
+  ArgsK k = (ArgsK)__builtin_amdgcn_kernarg_segment_ptr();
+  const LogicalBlock lb = xcd_block();   // one member's tiles per XCD (shared weights in L2)
+  bwd_body(m.a, lb.y, lb.x, lb.z, smem, nullptr, &k->u);
 }
 
 struct BwdMultiArgs {
@@ -798,6 +889,42 @@ DRPO_API int drpo_mlp_backward(const drpo_mlp_bwd_t* a, drpo_stream_t stream_) {
             a->trunk ? (a->split_heads ? a->nnets - 1 : 1) : a->nnets, a->nbatch);
   mlp_bwd_kernel<<<grid, FW_NT, bwd_lds(), stream>>>(*a);
   DRPO_LAUNCH_CHECK("mlp_backward");
+  return DRPO_OK;
+}
+
+DRPO_API int drpo_mlp_backward_ens(const drpo_mlp_bwd_t* a, const drpo_ens_upstream_t* up,
+                                   const drpo_ens_reduce_t* red_in, drpo_ens_reduce_t* reduce_out,
+                                   drpo_stream_t stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  DRPO_REQUIRE(a && up && red_in && reduce_out, "drpo_mlp_backward_ens: null argument");
+  DRPO_REQUIRE(a->upstream == DRPO_UPSTREAM_ENS && a->trunk && a->nnets == 3 && !a->split_heads &&
+                   a->nbatch == up->Z && a->rows == up->b,
+               "drpo_mlp_backward_ens: the descriptor must be the ensemble trunk + paired heads with upstream ENS");
+  const drpo_mlp_bwd_net_t &h1 = a->net[1], &h2 = a->net[2];
+  DRPO_REQUIRE(h1.nl == 2 && h2.nl == 2 && h1.L[1].dout == up->S + 1 && h2.L[1].dout == up->S + 1 &&
+                   up->S + 1 <= 64 && h1.L[1].act == ACT_NONE && h2.L[1].act == ACT_NONE &&
+                   (h1.L[0].dout == 200 || h1.L[0].dout == 256) && h1.L[0].dout == h2.L[0].dout &&
+                   h1.L[0].act == h2.L[0].act && !h1.dx && !h2.dx,
+               "drpo_mlp_backward_ens: heads must be paired [H -> 200|256 -> S+1] (S+1 <= 64)");
+  DRPO_REQUIRE(up->D && up->LVR && up->s && up->t && up->minlv && up->maxlv && up->part && up->b >= 1 &&
+                   up->Z >= 1 && up->Z <= 256,
+               "drpo_mlp_backward_ens: bad upstream");
+  for (int l = 0; l < a->net[0].nl; ++l)
+    DRPO_REQUIRE(a->net[0].L[l].din <= 256 && a->net[0].L[l].dout <= 256 && a->net[0].L[l].W,
+                 "drpo_mlp_backward_ens: bad trunk layer %d", l);
+  const int nbx = (int)((up->b + FW_ROWS - 1) / FW_ROWS);
+  *reduce_out = *red_in;
+  reduce_out->part = up->part;
+  reduce_out->nbx = nbx;
+  reduce_out->Z = up->Z;
+  reduce_out->S1 = up->S + 1;
+  reduce_out->minlv = up->minlv;
+  reduce_out->maxlv = up->maxlv;
+  reduce_out->gscale = up->gscale;
+  BwdEnsArgs m{*a, *up};
+  dim3 grid((unsigned)nbx, 1, a->nbatch);
+  mlp_bwd_ens_kernel<<<grid, FW_NT, bwd_lds(), stream>>>(m);
+  DRPO_LAUNCH_CHECK("mlp_backward_ens");
   return DRPO_OK;
 }
 

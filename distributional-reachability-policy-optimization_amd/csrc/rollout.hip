@@ -824,7 +824,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       tile_dense<NW, RB, MAXC, ACT_RELU>(h1, ldh, Ha, aW2, ab2, Ha, h2, ldh);
     }
     // the head's split-K share of wave w is k-steps w, w + NW, ...: exactly the hidden
-    // column blocks wave w just wrote (Ha <= 256), so no workgroup barrier here
+    // column blocks wave w just wrote (Ha <= 256), so no workgroup barrier here. That
+    // holds while tile_dense's column-block map (block wave + NW*c) and
+    // tile_dense_narrow_partials' k-step map (step wave + NW*q) are the same map and
+    // NW divides the 16 blocks of a 256-wide layer.
+    static_assert(16 % NW == 0, "wave-local head hand-off needs NW | 16");
     wave_lds_sync();
     if (t == 2) RSTAMP(3);
     // ---- actor head + squashed Gaussian sample + model input [normalize(s), a]:

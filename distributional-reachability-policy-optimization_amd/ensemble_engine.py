@@ -27,7 +27,7 @@ from . import _lib
 from .optim import fused_step
 from .rng import DeviceNoise
 from .sac_step import ACT_ID, Net, fill_bwd, fill_fwd
-from ._abi import EnsReduce, WgradItem
+from ._abi import EnsReduce, EnsUpstream, WgradItem
 
 
 # Forward: one workgroup per (row tile, head) when the plain grid (16-row tiles x
@@ -36,7 +36,9 @@ from ._abi import EnsReduce, WgradItem
 # dense layers: fit forward 28.8 -> 20.1 us at E=7, b=256 (csrc/mlp.hip, split_heads).
 # Backward: the same split (2 instead of 4 dense layers per workgroup, 33.8 -> 22.7 us)
 # leaves the trunk dZ as two terms, and the weight-gradient pass then re-reads the
-# trunk activations once per term (21 -> 38 us), so it is off unless DRPO_SPLIT_BWD=1.
+# trunk activations once per term (21 -> 38 us); measured and rejected in round 2. The
+# fit's backward now also forms the NLL gradients in-kernel from both heads' outputs
+# (drpo_mlp_backward_ens, paired heads), so the split backward is not offered.
 SPLIT_HEADS_MAX_TILES = 256
 
 
@@ -47,7 +49,7 @@ def split_heads(n, Z):
 
 
 def split_heads_bwd(n, Z):
-    return os.environ.get('DRPO_SPLIT_BWD', '0') == '1' and split_heads(n, Z)
+    return False
 
 
 class EnsembleEngine:
@@ -373,6 +375,19 @@ class EnsembleEngine:
         largs, _, gD, gL = self._loss_args(nets, xs, b * S, xt, b * S1, b, Z, True, loss_out=losses[0:1], tag='fit',
                                            bound=sh is None or sh.rank == 0)
         bd, wl = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
+        # the NLL loss rides in the backward launch (its output gradients formed in-kernel)
+        # and its reduction in the weight-gradient launch: forward, backward, wgrad, Adam
+        bd.upstream = 3   # DRPO_UPSTREAM_ENS
+        up = EnsUpstream()
+        up.D, up.LVR = nets[1].sy[-1].data_ptr(), nets[2].sy[-1].data_ptr()
+        up.s_zstride, up.t_zstride, up.b, up.S, up.Z = b * S, b * S1, b, S, Z
+        up.minlv, up.maxlv = m.min_log_var.data_ptr(), m.max_log_var.data_ptr()
+        up.part = self._loss_ws('fit', b, Z).data_ptr()
+        red_in = EnsReduce()
+        red_in.weight = float(m.log_var_bound_weight) if (sh is None or sh.rank == 0) else 0.0
+        red_in.mse = self.buf('fit.mse', Z).data_ptr()
+        red_in.gmin = g.view('min_log_var', g.grad).data_ptr()
+        red_in.gmax = g.view('max_log_var', g.grad).data_ptr()
         red = EnsReduce()
         full = E * b if sh is not None else rows
         idx_all = None
@@ -403,13 +418,12 @@ class EnsembleEngine:
                 _lib.check(L.drpo_ens_gather_steps(*gargs, nc, idx, nz.seed, ctr, S, A, _lib.ptr(cs), _lib.ptr(ca),
                                                    _lib.ptr(ct), stream), 'ens_gather')
             fd.src[0], fd.src[1] = cs.data_ptr() + 4 * k * rows * S, ca.data_ptr() + 4 * k * rows * A
-            largs[2] = ctypes.c_void_p(fd.src[0])
-            largs[4] = ctypes.c_void_p(ct.data_ptr() + 4 * k * rows * S1)
+            up.s, up.t = fd.src[0], ct.data_ptr() + 4 * k * rows * S1
+            red_in.loss = loss_base + 4 * i
             _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
-            largs[14] = ctypes.c_void_p(loss_base + 4 * i)
+            _lib.check(L.drpo_mlp_backward_ens(ctypes.byref(bd), ctypes.byref(up), ctypes.byref(red_in),
+                                               ctypes.byref(red), stream), 'ensemble backward')
             # the loss reduction rides as the last workgroup of the wgrad launch
-            _lib.check(L.drpo_ens_loss_partials(*largs, ctypes.byref(red), stream), 'ens_loss')
-            _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
             self._wgrad('fit', wl, red, stream)
             if sh is None:
                 self.dp.sum_(g.grad)
@@ -483,6 +497,9 @@ class EnsembleEngine:
         n = len(rb)
         S, A = m.state_dim, m.action_dim
         m.state_normalizer.fit(rb._states[:n])
+        # the same data-parallel contract as fit(steps=): one normalizer (rank 0's) on
+        # every replica, gradients sum-reduced with the 1/G in the optimizer
+        self.dp.broadcast_(m.state_normalizer.mean, m.state_normalizer.std)
         E, tb = m.ensemble_size, m.total_batch_size
         n_batches = -(-n // tb)
         losses = []
@@ -498,13 +515,15 @@ class EnsembleEngine:
                 ep_i = ep[bi:bi + 1].view(())
                 loss = self.compute_loss_value(xs, xa, xt, with_grads=True)
                 ep_i.copy_(loss)
-                self.dp.mean_(m.group.grad)
+                self.dp.sum_(m.group.grad)
+                # Adam (clipped on the reduced gradient's norm when asked) with the DP 1/G
+                # applied to the gradient and its norm inside the step
+                clip = None
                 if max_grad_norm is not None:
-                    part = grad_sumsq(m.group.grad)
-                    sc = m.optimizer.step_scalars()
-                    m.optimizer.apply(m.group.grad, 0, m.group.data.numel(), sc, clip=(part, max_grad_norm))
-                else:
-                    m.optimizer.step()
+                    clip = (grad_sumsq(m.group.grad), max_grad_norm)
+                sc = m.optimizer.step_scalars()
+                fused_step([m.optimizer.segment(0, m.group.size, sc, clip=clip, pack_map=m.group.pack_map(),
+                                                grad_scale=self.dp.scale)])
                 if post_step_callback is not None:
                     post_step_callback(epoch, bi, n_batches)
             losses.append(float(np.mean(ep.tolist())))

@@ -195,12 +195,31 @@ typedef struct {
   int upstream;        /* where the output gradients come from: DRPO_UPSTREAM_* */
 } drpo_mlp_bwd_t;
 
+/* The model fit's NLL loss (drpo_ens_loss's arithmetic, src/dynamics.py:136-153,236-253)
+ * as the upstream of the ensemble backward launch (drpo_mlp_backward_ens): the head
+ * outputs' gradients are formed in-kernel and the loss partials are left for the
+ * deferred reduction (drpo_mlp_wgrad_reduce). */
+typedef struct {
+  const float *D, *LVR;        /* diff / raw log-var head outputs [Z][b][S+1] */
+  const float* s;              /* raw states [Z][b][S] (member stride s_zstride) */
+  int64_t s_zstride;
+  const float* t;              /* targets [Z][b][S+1] */
+  int64_t t_zstride;
+  int64_t b;                   /* rows per member */
+  int S, Z;
+  const float *minlv, *maxlv;
+  const float* gscale;         /* optional device scale of the gradients (NULL = 1) */
+  float* part;                 /* loss workspace (drpo_ens_loss_workspace_size) */
+} drpo_ens_upstream_t;
+
 /* drpo_mlp_bwd_t.upstream */
 #define DRPO_UPSTREAM_GOUT 0     /* the nets' gout arrays */
 #define DRPO_UPSTREAM_CRITIC 1   /* twin-critic job: net k's output gradient is (q_k - y) / B with the soft
                                     Bellman target y of the launch's critic head; adds the critic loss */
 #define DRPO_UPSTREAM_CERT 2     /* constraint-critic job (trunk + mean [+ log-std] heads): the
                                     certificate loss gradients of the launch's critic head; adds its loss */
+#define DRPO_UPSTREAM_ENS 3      /* ensemble job (trunk + diff / log-var heads): the NLL gradients of the
+                                    launch's drpo_ens_upstream_t; writes its loss partials */
 
 typedef struct {
   const float* dz; /* [rows][dout] */
@@ -265,6 +284,12 @@ int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_
  * not written, loss[0] / loss[1] are accumulated) -- no separate head launch */
 int drpo_mlp_backward_multi_head(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
                                  const drpo_critic_head_t* head /* host */, drpo_stream_t stream);
+/* the model fit's backward with the NLL loss fused in: desc->upstream = DRPO_UPSTREAM_ENS,
+ * trunk + paired diff / log-var heads. reduce_out receives the deferred reduction
+ * (mse / loss / gmin / gmax / weight: from `red_in`, partial layout from this launch). */
+int drpo_mlp_backward_ens(const drpo_mlp_bwd_t* desc /* host */, const drpo_ens_upstream_t* up /* host */,
+                          const drpo_ens_reduce_t* red_in /* host */, drpo_ens_reduce_t* reduce_out,
+                          drpo_stream_t stream);
 /* Weight gradients of up to 16 layers (items) in ONE launch: gW += dZ^T Y, gb +=
  * colsum(dZ) (the autograd of nn.Linear / BatchedLinear, src/dynamics.py:26-52,
  * src/torch_util.py:190-211), split into (output tile x row chunk) workgroups whose
