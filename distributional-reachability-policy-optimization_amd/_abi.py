@@ -167,6 +167,15 @@ class BufferView(ctypes.Structure):
                 ('ptr_dev', P), ('cap', c_int64)]
 
 
+class ActorHead(ctypes.Structure):
+    """drpo_actor_head_t"""
+    _fields_ = [('B', c_int64), ('C', c_int), ('A', c_int), ('distributional', c_int), ('std_ratio', c_float),
+                ('log_std_min', c_float), ('log_std_max', c_float), ('lams', P), ('lam_upper_bound', c_float),
+                ('fixed_lam', c_float), ('clamp_lb', c_float), ('clamp_ub', c_float), ('u', P * 2), ('e', P * 2),
+                ('dA', P * 2), ('dA2', P * 2), ('logp', P), ('log_alpha', P), ('lp_scale', c_float),
+                ('target_entropy', c_float), ('alpha_sum', P)]
+
+
 class CriticHead(ctypes.Structure):
     """drpo_critic_head_t"""
     _fields_ = [('B', c_int64), ('C', c_int), ('distributional', c_int), ('deterministic_backup', c_int),
@@ -181,6 +190,7 @@ PROTOTYPES.update({
     'drpo_mlp_forward': (c_int, [POINTER(MlpFwd), P]),
     'drpo_mlp_forward_multi': (c_int, [POINTER(MlpFwd), P, c_int, c_uint64, c_uint64, P]),
     'drpo_mlp_backward_multi_head': (c_int, [POINTER(MlpBwd), P, c_int, POINTER(CriticHead), P]),
+    'drpo_mlp_backward_multi_actor': (c_int, [POINTER(MlpBwd), P, c_int, POINTER(ActorHead), P]),
     'drpo_mlp_backward_multi': (c_int, [POINTER(MlpBwd), P, c_int, P]),
     'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
     'drpo_mlp_backward_ens': (c_int, [POINTER(MlpBwd), POINTER(EnsUpstream), POINTER(EnsReduce), POINTER(EnsReduce),

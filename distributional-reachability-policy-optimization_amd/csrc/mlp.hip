@@ -652,10 +652,112 @@ __device__ __forceinline__ void ens_upstream(EnsUpK& u, const drpo_mlp_bwd_net_t
   }
 }
 
+// the actor update's head (drpo_mlp_backward_multi_actor), read in place from kernarg
+typedef const __attribute__((address_space(4))) drpo_actor_head_t ActorHeadK;
+
+// DRPO_UPSTREAM_ACTOR_CC / _SAFE_CC: the actor losses' gradient w.r.t. the constraint
+// critic's mean / raw log-std heads at (s, a) or (s, a_safe) (drpo_actor_upstream's
+// arithmetic, csrc/sac.hip; src/ssac.py:474-494): weight lam / B (actor) or 1 / B
+// (safe actor) on the arg-max constraint of the quantile bound mu + ratio * std; the
+// head outputs are the forward's saves (hm / hl last-layer sy). Gm / Gl (LDS) + the
+// output layers' saved dZ.
+__device__ __forceinline__ void actor_cc_upstream(ActorHeadK& h, int side, const drpo_mlp_bwd_net_t& hm,
+                                                  const drpo_mlp_bwd_net_t* hl, float* Gm, float* Gl, int row0,
+                                                  int nrows) {
+  const int C = h.C, opad = round_up(C, 16);
+  const bool dist = h.distributional;
+  const float* __restrict__ mu = hm.L[hm.nl - 1].sy;
+  const float* __restrict__ ls = hl ? hl->L[hl->nl - 1].sy : nullptr;
+  const float invB = 1.f / (float)h.B;
+  for (int e = threadIdx.x; e < FW_ROWS * opad; e += FW_NT) {
+    const int r = e / opad, k = e - r * opad;
+    float gm = 0.f, gs = 0.f;
+    if (r < nrows && k < C) {
+      const int64_t i = row0 + r;
+      float best = 0.f, lbest = 0.f;
+      int bi = 0;
+      for (int c = 0; c < C; ++c) {
+        float v = mu[i * C + c];
+        const float l = dist ? ls[i * C + c] : 0.f;
+        if (dist) v = v + h.std_ratio * cc_std(l, h.log_std_min, h.log_std_max);
+        if (c == 0 || v > best) { best = v; bi = c; lbest = l; }
+      }
+      float g = invB;
+      if (side == 0) {
+        float lam = h.lams ? h.lams[i] : h.fixed_lam;
+        const float ub = h.lam_upper_bound;
+        if (h.lams && ub > 0.f) lam = ub / 2.f * (1.f + tanhf(lam / ub * 2.f));   // MLPMultiplier.forward
+        if (!h.lams && (best < h.clamp_lb || best > h.clamp_ub)) lam = 0.f;       // clamped scalar-lam term
+        g = lam * invB;
+      }
+      float gl = 0.f;
+      if (dist && g != 0.f) {
+        const float sd = cc_std(lbest, h.log_std_min, h.log_std_max);
+        gl = g * h.std_ratio * cc_dstd_draw(lbest, h.log_std_min, h.log_std_max, sd);
+      }
+      gm = k == bi ? g : 0.f;
+      gs = k == bi ? gl : 0.f;
+      const size_t o = (size_t)i * C + k;
+      if (hm.L[hm.nl - 1].dz) gstore(hm.L[hm.nl - 1].dz + o, gm);
+      if (hl && hl->L[hl->nl - 1].dz) gstore(hl->L[hl->nl - 1].dz + o, gs);
+    }
+    Gm[r * LDH + k] = gm;
+    if (Gl) Gl[r * LDH + k] = gs;
+  }
+}
+
+// DRPO_UPSTREAM_SQUASH / _SQUASH_SAFE: the chain rule through rsample + tanh + log_prob
+// of the squashed Gaussian (drpo_squash_backward's arithmetic, csrc/sac.hip;
+// src/policy.py:89-97, src/ssac.py:458-505) to the net's raw [mu | log-std] outputs
+// (the forward's save), and the alpha-loss sum for the actor
+__device__ __forceinline__ void squash_upstream(ActorHeadK& h, int side, const drpo_mlp_bwd_net_t& n, float* G,
+                                                int row0, int nrows) {
+  const int A = h.A;
+  const float* __restrict__ raw = n.L[n.nl - 1].sy;
+  const float* __restrict__ u = h.u[side];
+  const float* __restrict__ ep = h.e[side];
+  const float* __restrict__ dA = h.dA[side];
+  const float* __restrict__ dA2 = h.dA2[side];
+  const float glp = (side == 0 && h.log_alpha) ? expf(*h.log_alpha) * h.lp_scale : 0.f;
+  float asum = 0.f;
+  for (int e = threadIdx.x; e < FW_ROWS * 16; e += FW_NT) {
+    const int r = e >> 4, k = e & 15;
+    float gv = 0.f;
+    if (r < nrows && k < 2 * A) {
+      const int64_t i = row0 + r;
+      const int d = k < A ? k : k - A;
+      const float mu = raw[i * 2 * A + d], rr = raw[i * 2 * A + A + d];
+      const float uu = u[i * A + d], ee = ep[i * A + d];
+      const float dAv = dA2 ? dA[i * A + d] + dA2[i * A + d] : dA[i * A + d];
+      const float sg = sigmoidf(rr);
+      const float sd = expf(-6.f + 10.f * sg) * 1.0f;
+      const float a = tanhf(uu);
+      const float diff = uu - mu;
+      const float var = sd * sd;
+      const float du = dAv * (1.f - a * a) + glp * (-diff / var + 2.f - 4.f * sp_grad(-2.f * uu));
+      if (k < A) {
+        gv = du + glp * diff / var;
+      } else {
+        const float dsd = du * ee + glp * (diff * diff / (var * sd) - 1.f / sd);
+        gv = dsd * sd * 10.f * sg * (1.f - sg);
+      }
+      if (side == 0 && h.alpha_sum && k == 0) asum = h.logp[i] + h.target_entropy;
+    }
+    G[r * LDH + k] = gv;
+  }
+  if (side == 0 && h.alpha_sum) wave_loss_add(asum, h.alpha_sum);
+}
+
+// upstream families compiled into a backward kernel instantiation (each launch kind
+// gets only the producer code it uses, so none of them adds register pressure -- and
+// spills -- to the others' GEMM phases)
+constexpr int UPF_CRITIC = 1, UPF_ENS = 2, UPF_ACTOR = 4;
+
 // heads' output gradients -> trunk-output gradient in G (bA, bB, DT are scratch)
+template <int UPF>
 __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restrict__ a, float* G, float* bA, float* bB,
                                                  float* DT, int z, int row0, int nrows, CriticHeadK* ch,
-                                                 EnsUpK* eu = nullptr) {
+                                                 EnsUpK* eu = nullptr, ActorHeadK* ah = nullptr) {
   const int tid = threadIdx.x;
   const drpo_mlp_bwd_net_t &h1 = a.net[1], &h2 = a.net[2];
   const int hid = h1.L[0].dout, out = h1.L[1].dout;
@@ -664,9 +766,17 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
   bwd_fetch_act(h1.L[0], z, a.rows, row0, nrows, sv1);   // head 1's hidden saved values, one phase ahead
   // output layers (identity): dZ = the given output gradient, saved for the weight gradients
   const size_t so = ((size_t)z * a.rows + row0) * out;
-  if (eu) ens_upstream(*eu, h1, h2, G, bA, bB, DT, z, row0 / FW_ROWS, row0, nrows);
-  else if (ch) cert_upstream(*ch, h1, &h2, G, bA, row0, nrows);
-  else
+  bool done = false;
+  if constexpr ((UPF & UPF_ENS) != 0) {
+    if (eu) { ens_upstream(*eu, h1, h2, G, bA, bB, DT, z, row0 / FW_ROWS, row0, nrows); done = true; }
+  }
+  if constexpr ((UPF & UPF_CRITIC) != 0) {
+    if (ch) { cert_upstream(*ch, h1, &h2, G, bA, row0, nrows); done = true; }
+  }
+  if constexpr ((UPF & UPF_ACTOR) != 0) {
+    if (ah) { actor_cc_upstream(*ah, a.upstream == DRPO_UPSTREAM_SAFE_CC, h1, &h2, G, bA, row0, nrows); done = true; }
+  }
+  if (!done)
   for (int e = tid; e < 2 * FW_ROWS * opad; e += FW_NT) {
     const int w = e / (FW_ROWS * opad), e2 = e - w * FW_ROWS * opad;
     const int r = e2 / opad, k = e2 - r * opad;
@@ -719,8 +829,9 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
 
 // one (job, net) slot of the fused backward-data pass; `a` may live in kernarg
 // (single launch) or global memory (multi-job launch)
+template <int UPF>
 __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, int sel, int bx, int bz, float* smem,
-                                         CriticHeadK* ch = nullptr, EnsUpK* eu = nullptr) {
+                                         CriticHeadK* ch = nullptr, EnsUpK* eu = nullptr, ActorHeadK* ah = nullptr) {
   float* G = smem;
   float* bA = G + FW_ROWS * LDH;
   float* bB = bA + FW_ROWS * LDH;
@@ -751,8 +862,13 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
   };
 
   // output gradients formed in-kernel from the launch's critic head (no head launch)
+  if constexpr ((UPF & UPF_CRITIC) == 0) ch = nullptr;
+  if constexpr ((UPF & UPF_ENS) == 0) eu = nullptr;
+  if constexpr ((UPF & UPF_ACTOR) == 0) ah = nullptr;
   CriticHeadK* hq = (ch && a.upstream == DRPO_UPSTREAM_CRITIC) ? ch : nullptr;
   CriticHeadK* hc = (ch && a.upstream == DRPO_UPSTREAM_CERT) ? ch : nullptr;
+  const bool acc_up = a.upstream == DRPO_UPSTREAM_ACTOR_CC || a.upstream == DRPO_UPSTREAM_SAFE_CC;
+  ActorHeadK* ha = (ah && acc_up) ? ah : nullptr;
   if (!a.trunk) {
     const drpo_mlp_bwd_net_t& n = a.net[sel];
     if (hq) {
@@ -774,6 +890,16 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
       }
       wave_loss_add(lq, hq->loss);
       lds_barrier();
+    } else if (ah && a.upstream == DRPO_UPSTREAM_NEG_MEAN) {
+      // the actor loss's -mean(Q_k) (src/ssac.py:472): dL/dQ = -1/B
+      for (int e = tid; e < FW_ROWS * 16; e += FW_NT) {
+        const int r = e >> 4, k = e & 15;
+        G[r * LDH + k] = (r < nrows && k == 0) ? -1.f / (float)ah->B : 0.f;
+      }
+      lds_barrier();
+    } else if (ah && (a.upstream == DRPO_UPSTREAM_SQUASH || a.upstream == DRPO_UPSTREAM_SQUASH_SAFE)) {
+      squash_upstream(*ah, a.upstream == DRPO_UPSTREAM_SQUASH_SAFE, n, G, row0, nrows);
+      lds_barrier();
     } else {
       load_gout(n, G);
     }
@@ -791,7 +917,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     return;
   }
   if (bwd_paired_heads(a)) {
-    bwd_heads_paired(a, G, bA, bB, DT, z, row0, nrows, hc, a.upstream == DRPO_UPSTREAM_ENS ? eu : nullptr);
+    bwd_heads_paired<UPF>(a, G, bA, bB, DT, z, row0, nrows, hc, a.upstream == DRPO_UPSTREAM_ENS ? eu : nullptr, ha);
     const float* gx = bwd_net(a.net[0], G, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
     if (gx) store_dx(a.net[0], gx);
     return;
@@ -804,6 +930,9 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
   for (int h = 1; h < a.nnets; ++h) {
     if (hc && h == 1) {      // vanilla certificate: the mean head only (src/ssac.py:426-435)
       cert_upstream(*hc, a.net[1], nullptr, G, nullptr, row0, nrows);
+      lds_barrier();
+    } else if (ha && h == 1) {   // vanilla: the mean head only
+      actor_cc_upstream(*ha, a.upstream == DRPO_UPSTREAM_SAFE_CC, a.net[1], nullptr, G, nullptr, row0, nrows);
       lds_barrier();
     } else {
       load_gout(a.net[h], G);
@@ -827,7 +956,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_kernel(drpo_mlp_bwd_t a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const LogicalBlock lb = xcd_block();   // one member's tiles per XCD (shared weights in L2)
-  bwd_body(a, lb.y, lb.x, lb.z, smem);
+  bwd_body<0>(a, lb.y, lb.x, lb.z, smem);
 }
 
 // the model fit's backward with the NLL loss fused in (one workgroup per (row tile,
@@ -842,16 +971,18 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   typedef const __attribute__((address_space(4))) BwdEnsArgs* ArgsK;
   ArgsK k = (ArgsK)__builtin_amdgcn_kernarg_segment_ptr();
   const LogicalBlock lb = xcd_block();   // one member's tiles per XCD (shared weights in L2)
-  bwd_body(m.a, lb.y, lb.x, lb.z, smem, nullptr, &k->u);
+  bwd_body<UPF_ENS>(m.a, lb.y, lb.x, lb.z, smem, nullptr, &k->u);
 }
 
 struct BwdMultiArgs {
   const drpo_mlp_bwd_t* jobs;
   unsigned char slot_job[16], slot_net[16];
-  int has_head;
+  int has_head, has_actor;
   drpo_critic_head_t head;
+  drpo_actor_head_t actor;
 };
 
+template <int UPF>
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void mlp_bwd_multi_kernel(
     BwdMultiArgs m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -860,7 +991,8 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   if (blockIdx.z >= (unsigned)a.nbatch) return;
   typedef const __attribute__((address_space(4))) BwdMultiArgs* ArgsK;
   ArgsK k = (ArgsK)__builtin_amdgcn_kernarg_segment_ptr();
-  bwd_body(a, m.slot_net[blockIdx.y], blockIdx.x, blockIdx.z, smem, m.has_head ? &k->head : nullptr);
+  bwd_body<UPF>(a, m.slot_net[blockIdx.y], blockIdx.x, blockIdx.z, smem, m.has_head ? &k->head : nullptr, nullptr,
+                m.has_actor ? &k->actor : nullptr);
 }
 
 static size_t bwd_lds() { return sizeof(float) * (size_t)4 * FW_ROWS * LDH; }
@@ -945,12 +1077,30 @@ DRPO_API int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo
   return drpo_mlp_backward_multi_head(jobs_host, jobs_dev, njobs, nullptr, stream_);
 }
 
+static int bwd_multi_launch(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                            const drpo_critic_head_t* head, const drpo_actor_head_t* actor, hipStream_t stream);
+
 DRPO_API int drpo_mlp_backward_multi_head(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
                                           const drpo_critic_head_t* head, drpo_stream_t stream_) {
-  hipStream_t stream = (hipStream_t)stream_;
+  return bwd_multi_launch(jobs_host, jobs_dev, njobs, head, nullptr, (hipStream_t)stream_);
+}
+
+DRPO_API int drpo_mlp_backward_multi_actor(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                                           const drpo_actor_head_t* actor, drpo_stream_t stream_) {
+  DRPO_REQUIRE(actor && actor->B >= 0 && actor->A >= 1 && actor->A <= 8 && actor->C >= 1 && actor->C <= 16,
+               "drpo_mlp_backward_multi_actor: bad actor head");
+  return bwd_multi_launch(jobs_host, jobs_dev, njobs, nullptr, actor, (hipStream_t)stream_);
+}
+
+static int bwd_multi_launch(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                            const drpo_critic_head_t* head, const drpo_actor_head_t* actor, hipStream_t stream) {
   DRPO_REQUIRE(jobs_host && jobs_dev && njobs >= 1 && njobs <= 8, "drpo_mlp_backward_multi: 1..8 jobs");
   BwdMultiArgs m{};
   m.jobs = jobs_dev;
+  if (actor) {
+    m.has_actor = 1;
+    m.actor = *actor;
+  }
   if (head) {
     DRPO_REQUIRE(head->C >= 1 && head->B >= 0 && head->loss && head->log_alpha && head->q0 && head->q1 && head->mu,
                  "drpo_mlp_backward_multi_head: bad critic head");
@@ -959,9 +1109,29 @@ DRPO_API int drpo_mlp_backward_multi_head(const drpo_mlp_bwd_t* jobs_host, const
   }
   for (int j = 0; j < njobs; ++j) {
     const drpo_mlp_bwd_t& J = jobs_host[j];
-    DRPO_REQUIRE(J.upstream >= DRPO_UPSTREAM_GOUT && J.upstream <= DRPO_UPSTREAM_CERT,
+    DRPO_REQUIRE(J.upstream >= DRPO_UPSTREAM_GOUT && J.upstream <= DRPO_UPSTREAM_SQUASH_SAFE &&
+                     J.upstream != DRPO_UPSTREAM_ENS,
                  "drpo_mlp_backward_multi: job %d upstream %d", j, J.upstream);
     if (J.upstream == DRPO_UPSTREAM_GOUT) continue;
+    if (J.upstream >= DRPO_UPSTREAM_ACTOR_CC) {
+      DRPO_REQUIRE(actor && J.nbatch == 1 && J.rows == actor->B, "drpo_mlp_backward_multi: job %d needs the actor head",
+                   j);
+      const drpo_mlp_bwd_net_t& n0 = J.net[0];
+      if (J.upstream == DRPO_UPSTREAM_NEG_MEAN)
+        DRPO_REQUIRE(!J.trunk && J.nnets == 1 && n0.L[n0.nl - 1].dout == 1,
+                     "drpo_mlp_backward_multi: job %d: -1/B upstream needs one single-output net", j);
+      else if (J.upstream >= DRPO_UPSTREAM_SQUASH)
+        DRPO_REQUIRE(!J.trunk && J.nnets == 1 && n0.L[n0.nl - 1].dout == 2 * actor->A && n0.L[n0.nl - 1].sy &&
+                         actor->u[J.upstream - DRPO_UPSTREAM_SQUASH] && actor->e[J.upstream - DRPO_UPSTREAM_SQUASH] &&
+                         actor->dA[J.upstream - DRPO_UPSTREAM_SQUASH],
+                     "drpo_mlp_backward_multi: job %d: squash upstream needs the policy net and its samples", j);
+      else
+        DRPO_REQUIRE(J.trunk && J.nnets >= 2 && J.net[1].L[J.net[1].nl - 1].dout == actor->C &&
+                         J.net[1].L[J.net[1].nl - 1].sy &&
+                         (!actor->distributional || (J.nnets == 3 && J.net[2].L[J.net[2].nl - 1].sy)),
+                     "drpo_mlp_backward_multi: job %d: constraint-critic upstream needs its saved head outputs", j);
+      continue;
+    }
     DRPO_REQUIRE(head && J.nbatch == 1 && J.rows == head->B, "drpo_mlp_backward_multi: job %d needs the critic head", j);
     if (J.upstream == DRPO_UPSTREAM_CRITIC)
       DRPO_REQUIRE(!J.trunk && J.nnets == 2 && J.net[0].L[J.net[0].nl - 1].dout == 1 &&
@@ -988,7 +1158,13 @@ DRPO_API int drpo_mlp_backward_multi_head(const drpo_mlp_bwd_t* jobs_host, const
     nbatch = max(nbatch, a->nbatch);
   }
   if (tiles == 0) return DRPO_OK;
-  mlp_bwd_multi_kernel<<<dim3((unsigned)tiles, slots, nbatch), FW_NT, bwd_lds(), stream>>>(m);
+  const dim3 grid((unsigned)tiles, slots, nbatch);
+  if (m.has_head)
+    mlp_bwd_multi_kernel<UPF_CRITIC><<<grid, FW_NT, bwd_lds(), stream>>>(m);
+  else if (m.has_actor)
+    mlp_bwd_multi_kernel<UPF_ACTOR><<<grid, FW_NT, bwd_lds(), stream>>>(m);
+  else
+    mlp_bwd_multi_kernel<0><<<grid, FW_NT, bwd_lds(), stream>>>(m);
   DRPO_LAUNCH_CHECK("mlp_backward_multi");
   return DRPO_OK;
 }

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._abi import (BufferView, CriticHead, MlpBwd, MlpFwd, WgradItem)
+from ._abi import (ActorHead, BufferView, CriticHead, MlpBwd, MlpFwd, WgradItem)
 from .optim import ema_segment, fused_step, grad_sumsq_multi
 
 ACT_ID = {None: 0, 'identity': 0, 'relu': 1, 'swish': 2, 'tanh': 3}
@@ -94,7 +94,9 @@ def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, ws
     return d
 
 
-UPSTREAM_GOUT, UPSTREAM_CRITIC, UPSTREAM_CERT = 0, 1, 2   # drpo_mlp_bwd_t.upstream
+# drpo_mlp_bwd_t.upstream (include/drpo_hip.h DRPO_UPSTREAM_*)
+UPSTREAM_GOUT, UPSTREAM_CRITIC, UPSTREAM_CERT, UPSTREAM_ENS = 0, 1, 2, 3
+UPSTREAM_ACTOR_CC, UPSTREAM_SAFE_CC, UPSTREAM_NEG_MEAN, UPSTREAM_SQUASH, UPSTREAM_SQUASH_SAFE = 4, 5, 6, 7, 8
 
 
 def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None, split_heads=False, upstream=0):
@@ -371,7 +373,7 @@ class SACEngine:
         if ev:
             self.profiler.end(ev)
 
-    def _run_bwd_multi(self, key, builder, head=None):
+    def _run_bwd_multi(self, key, builder, head=None, actor=None):
         d = self.desc.get(key)
         if d is None:
             jobs = builder()
@@ -379,7 +381,10 @@ class SACEngine:
             d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(bwd_flops(j) for j in jobs))
         arr, dev, nj, fl = d
         ev = self.profiler.begin('mlp_bwd', key, fl) if self.profiler else None
-        if head is None:
+        if actor is not None:
+            _lib.check(_lib.lib().drpo_mlp_backward_multi_actor(arr, dev.data_ptr(), nj, ctypes.byref(actor),
+                                                                _lib.stream()), key)
+        elif head is None:
             _lib.check(_lib.lib().drpo_mlp_backward_multi(arr, dev.data_ptr(), nj, _lib.stream()), key)
         else:
             _lib.check(_lib.lib().drpo_mlp_backward_multi_head(arr, dev.data_ptr(), nj, ctypes.byref(head),
@@ -645,46 +650,49 @@ class SACEngine:
             self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
             self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
                                                      [(self.bs, S), (sqc, 1), (None, 0)], B))
-        # upstream gradients; lam = MLPMultiplier's output transform of 'a.multx', applied
-        # inside actor_upstream (no separate multiplier_out launch) -- or, with the scalar
-        # multiplier, lam = fixed_multiplier on clamp(Qc, penalty_lb, penalty_ub)
-        # (src/ssac.py:480-484)
-        ca, cs = self._cc_views('a.cc'), self._cc_views('a.cc2')
-        gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
-                                    self.buf('a.gmu2', B, C), self.buf('a.gls2', B, C))
-        ub = float(sol.mlp_multiplier_cfg.upper_bound)
-        assert ub > 0 or not mlp_mult, 'MLPMultiplier upper_bound must be positive'
-        _lib.check(L.drpo_actor_upstream(B, C, int(dist), float(cc.std_ratio), float(cc.log_std_min),
-                                         float(cc.log_std_max), ws['a.multx'].data_ptr() if mlp_mult else None,
-                                         ca[0].data_ptr(), ca[1].data_ptr(), cs[0].data_ptr(), cs[1].data_ptr(),
-                                         gq.data_ptr(), gmu.data_ptr(), gls.data_ptr(), gmu2.data_ptr(),
-                                         gls2.data_ptr(), ub, float(sol.fixed_multiplier), float(sol.penalty_lb),
-                                         float(sol.penalty_ub), _lib.stream()),
-                   'actor_upstream')
-        # dL/da of the actor (Q_k part + certificate part, summed in squash_backward in
+        # The actor losses' output gradients are formed inside the two backward launches
+        # (drpo_actor_head_t): w.r.t. Q_k (-1/B) and the constraint critic's heads at (s, a)
+        # (lam / B on the max-C bound; lam = MLPMultiplier's output transform of 'a.multx',
+        # or the scalar multiplier on clamp(Qc, penalty_lb, penalty_ub), src/ssac.py:474-494)
+        # and at (s, a_safe) (1 / B), then the squashed-Gaussian backward of both actors
+        # and the alpha-loss sum (src/ssac.py:458-505) -- no separate head launches.
+        ah = self.desc.get('a.head')
+        if ah is None:
+            ah = self.desc['a.head'] = ActorHead()
+            ub = float(sol.mlp_multiplier_cfg.upper_bound)
+            assert ub > 0 or not mlp_mult, 'MLPMultiplier upper_bound must be positive'
+            ah.B, ah.C, ah.A, ah.distributional = B, C, A, int(dist)
+            ah.std_ratio, ah.log_std_min, ah.log_std_max = float(cc.std_ratio), float(cc.log_std_min), \
+                float(cc.log_std_max)
+            ah.lams = ws['a.multx'].data_ptr() if mlp_mult else 0
+            ah.lam_upper_bound, ah.fixed_lam = ub, float(sol.fixed_multiplier)
+            ah.clamp_lb, ah.clamp_ub = float(sol.penalty_lb), float(sol.penalty_ub)
+            ah.u[0], ah.e[0], ah.u[1], ah.e[1] = u.data_ptr(), e.data_ptr(), u_s.data_ptr(), e_s.data_ptr()
+            ah.dA[0], ah.dA2[0], ah.dA[1] = self.buf('a.dA', B, A).data_ptr(), self.buf('a.dAc', B, A).data_ptr(), \
+                self.buf('a.dAs', B, A).data_ptr()
+            ah.logp, ah.log_alpha, ah.lp_scale = lp.data_ptr(), sol.log_alpha.data_ptr(), 1.0 / B
+            ah.target_entropy = float(sol.target_entropy)
+            ah.alpha_sum = self.alpha_sum.data_ptr() if sol.autotune_alpha else 0
+        # dL/da of the actor (Q_k part + certificate part, summed in the squash backward in
         # the reference's order) and of the safe actor: one backward launch
         dA, dAc, dAs = self.buf('a.dA', B, A), self.buf('a.dAc', B, A), self.buf('a.dAs', B, A)
         hv, hv2 = self.nets_view['a.cc'], self.nets_view['a.cc2']
+        gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
+                                    self.buf('a.gmu2', B, C), self.buf('a.gls2', B, C))
         self._run_bwd_multi(f'a.b.{k}{int(dist)}', lambda: [
             fill_bwd(hv if dist else hv[:2], [None, gmu, gls][:3 if dist else 2], B, trunk=True,
-                     dx={0: (dAc, S, A, False)}),
+                     dx={0: (dAc, S, A, False)}, upstream=UPSTREAM_ACTOR_CC),
             fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B, trunk=True,
-                     dx={0: (dAs, S, A, False)}),
-            fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)})])
-        # squashed Gaussian backward -> actor heads; alpha loss sum (exchange-arena slot)
-        asum = self.alpha_sum
+                     dx={0: (dAs, S, A, False)}, upstream=UPSTREAM_SAFE_CC),
+            fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)}, upstream=UPSTREAM_NEG_MEAN)],
+            actor=ah)
         draw, draws = self.buf('a.draw', B, 2 * A), self.buf('a.draws', B, 2 * A)
-        _lib.check(L.drpo_squash_backward(B, A, raw.data_ptr(), u.data_ptr(), e.data_ptr(), dA.data_ptr(),
-                                          dAc.data_ptr(), sol.log_alpha.data_ptr(), 1.0 / B, lp.data_ptr(),
-                                          float(sol.target_entropy), asum.data_ptr() if sol.autotune_alpha else None,
-                                          draw.data_ptr(),
-                                          _lib.stream()), 'squash_backward')
-        _lib.check(L.drpo_squash_backward(B, A, raws.data_ptr(), u_s.data_ptr(), e_s.data_ptr(), dAs.data_ptr(),
-                                          None, None, 0.0, None, 0.0, None, draws.data_ptr(), _lib.stream()),
-                   'squash_backward_safe')
+        asum = self.alpha_sum
         self._clean_grads(sol.actor.group)
         self._clean_grads(sol.actor_safe.group)
-        self._run_bwd_multi('a.bpi', lambda: [fill_bwd([n['actor']], [draw], B), fill_bwd([n['safe']], [draws], B)])
+        self._run_bwd_multi('a.bpi', lambda: [fill_bwd([n['actor']], [draw], B, upstream=UPSTREAM_SQUASH),
+                                              fill_bwd([n['safe']], [draws], B, upstream=UPSTREAM_SQUASH_SAFE)],
+                            actor=ah)
         na, ns = n['actor'], n['safe']
         sq = self._sq('a', ('a', 's'))
         used = self._run_wgrad('a.wg' + ('f' if sq else ''),

@@ -212,6 +212,25 @@ typedef struct {
   float* part;                 /* loss workspace (drpo_ens_loss_workspace_size) */
 } drpo_ens_upstream_t;
 
+/* The actor update's output gradients (src/ssac.py:458-527), formed in-kernel by its
+ * backward launches (drpo_mlp_backward_multi_actor): what drpo_actor_upstream and
+ * drpo_squash_backward compute as separate launches. */
+typedef struct {
+  int64_t B;
+  int C, A, distributional;
+  float std_ratio, log_std_min, log_std_max;
+  const float* lams;            /* MLPMultiplier pre-transform outputs [B], or NULL: fixed_lam */
+  float lam_upper_bound, fixed_lam, clamp_lb, clamp_ub;
+  const float* u[2];            /* pre-tanh samples of the actor [0] / safe actor [1] [B][A] */
+  const float* e[2];            /* their standard-normal draws [B][A] */
+  const float* dA[2];           /* dL/d action [B][A] */
+  const float* dA2[2];          /* optional second term of dL/d action (NULL) */
+  const float* logp;            /* actor log-probs [B] */
+  const float* log_alpha;       /* the actor's log-prob terms scaled by exp(*log_alpha) * lp_scale; NULL: none */
+  float lp_scale, target_entropy;
+  float* alpha_sum;             /* += sum(logp + target_entropy) (actor), or NULL */
+} drpo_actor_head_t;
+
 /* drpo_mlp_bwd_t.upstream */
 #define DRPO_UPSTREAM_GOUT 0     /* the nets' gout arrays */
 #define DRPO_UPSTREAM_CRITIC 1   /* twin-critic job: net k's output gradient is (q_k - y) / B with the soft
@@ -220,6 +239,13 @@ typedef struct {
                                     certificate loss gradients of the launch's critic head; adds its loss */
 #define DRPO_UPSTREAM_ENS 3      /* ensemble job (trunk + diff / log-var heads): the NLL gradients of the
                                     launch's drpo_ens_upstream_t; writes its loss partials */
+#define DRPO_UPSTREAM_ACTOR_CC 4 /* constraint critic at (s, a): lam / B on the max-C certificate bound of
+                                    the launch's drpo_actor_head_t (src/ssac.py:474-488) */
+#define DRPO_UPSTREAM_SAFE_CC 5  /* constraint critic at (s, a_safe): 1 / B on its max-C bound (:490-494) */
+#define DRPO_UPSTREAM_NEG_MEAN 6 /* single net with one output: -1 / B (the actor loss's -mean(Q_k)) */
+#define DRPO_UPSTREAM_SQUASH 7   /* actor (net 0 of the launch's head: [0]) / safe actor ([1]): the
+                                    squashed-Gaussian backward of the head's action gradients */
+#define DRPO_UPSTREAM_SQUASH_SAFE 8
 
 typedef struct {
   const float* dz; /* [rows][dout] */
@@ -284,6 +310,9 @@ int drpo_mlp_backward_multi(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_
  * not written, loss[0] / loss[1] are accumulated) -- no separate head launch */
 int drpo_mlp_backward_multi_head(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
                                  const drpo_critic_head_t* head /* host */, drpo_stream_t stream);
+/* the actor update's backward launches with actor_upstream / squash_backward fused in */
+int drpo_mlp_backward_multi_actor(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_t* jobs_dev, int njobs,
+                                  const drpo_actor_head_t* head /* host */, drpo_stream_t stream);
 /* the model fit's backward with the NLL loss fused in: desc->upstream = DRPO_UPSTREAM_ENS,
  * trunk + paired diff / log-var heads. reduce_out receives the deferred reduction
  * (mse / loss / gmin / gmax / weight: from `red_in`, partial layout from this launch). */
