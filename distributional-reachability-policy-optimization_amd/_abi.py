@@ -49,7 +49,7 @@ class OptimSeg(ctypes.Structure):
                 ('eps', c_float), ('weight_decay', c_float), ('zero_grad', c_int),
                 ('ema_target', P), ('ema_rate', c_float), ('ema_keep', c_float), ('map', P),
                 ('grad_from_sum', P), ('grad_sum_rows', c_int64), ('grad_from_sum_kind', c_int),
-                ('grad_scale', c_float)]
+                ('grad_scale', c_float), ('grad_sum_n', c_int)]
 
 
 class EnsReduce(ctypes.Structure):
@@ -183,7 +183,12 @@ class CriticHead(ctypes.Structure):
                 ('log_alpha', P), ('r', P), ('h', P), ('d', P), ('dc', P), ('q0t', P), ('q1t', P), ('logp2', P),
                 ('mu_t', P), ('ls_t', P), ('eps3', P), ('seed', c_uint64), ('ctr', c_uint64),
                 ('q0', P), ('q1', P), ('mu', P), ('ls', P), ('dq0', P), ('dq1', P), ('dmu', P), ('dls', P),
-                ('loss', P)]
+                ('loss', P), ('loss_part', P)]
+
+
+class SumDesc(ctypes.Structure):
+    """drpo_sum_t"""
+    _fields_ = [('part', P), ('n', c_int), ('out', P)]
 
 
 PROTOTYPES.update({
@@ -199,6 +204,7 @@ PROTOTYPES.update({
     'drpo_mlp_wgrad_tiles': (c_int, [POINTER(WgradItem)]),
     'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P, c_size_t, P]),
     'drpo_mlp_wgrad_reduce': (c_int, [POINTER(WgradItem), c_int, POINTER(EnsReduce), P, c_size_t, P]),
+    'drpo_mlp_wgrad_sums': (c_int, [POINTER(WgradItem), c_int, POINTER(SumDesc), c_int, P, c_size_t, P]),
     'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
                                   c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
     'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,

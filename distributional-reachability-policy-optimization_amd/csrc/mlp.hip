@@ -547,19 +547,30 @@ __device__ __forceinline__ void bwd_heads_out(const drpo_mlp_bwd_net_t& h1, cons
 // would copy it to scratch)
 typedef const __attribute__((address_space(4))) drpo_critic_head_t CriticHeadK;
 
-// a loss partial of every thread of the workgroup -> one float atomic per wave
-__device__ __forceinline__ void wave_loss_add(float v, float* dst) {
+// a loss partial of every thread of the workgroup -> the workgroup's sum written to
+// *dst (one slot per workgroup, no atomics; waves summed in order; every thread calls)
+__device__ __forceinline__ void wg_loss_partial(float v, float* dst) {
+  __shared__ float s_wl[FW_NW];
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(dst, v);
+  if ((threadIdx.x & 63) == 0) s_wl[threadIdx.x >> 6] = v;
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < FW_NW; ++w) t += s_wl[w];
+    *dst = t;
+  }
 }
 
 // DRPO_UPSTREAM_CERT: the certificate loss gradients of rows [row0, row0+nrows)
 // (cert_element, src/ssac.py:304-435) as the mean / log-std heads' output gradients:
-// dmu -> Gm, dls -> Gl (LDS, width padded to 16), saved as the heads' output-layer dZ;
+// dmu -> Gm, dls -> Gl (LDS, width padded to 16; either may be NULL: the generic trunk
+// path takes one head at a time), saved as that head's output-layer dZ; with add_loss
 // the loss term is accumulated into head->loss[1]
-__device__ __forceinline__ void cert_upstream(CriticHeadK& ch, const drpo_mlp_bwd_net_t& hm,
+__device__ __forceinline__ void cert_upstream(CriticHeadK& ch, const drpo_mlp_bwd_net_t* hm,
                                               const drpo_mlp_bwd_net_t* hl, float* Gm, float* Gl, int row0,
-                                              int nrows) {
+                                              int nrows, bool add_loss) {
+  const int tiles = (int)((ch.B + FW_ROWS - 1) / FW_ROWS);
   const int C = ch.C, opad = round_up(C, 16);
   float lc = 0.f;
   for (int e = threadIdx.x; e < FW_ROWS * opad; e += FW_NT) {
@@ -569,13 +580,13 @@ __device__ __forceinline__ void cert_upstream(CriticHeadK& ch, const drpo_mlp_bw
       const int64_t i = row0 + r;
       lc += cert_element(ch, i, k, dmu, dls);
       const size_t o = (size_t)i * C + k;
-      if (hm.L[hm.nl - 1].dz) gstore(hm.L[hm.nl - 1].dz + o, dmu);
-      if (hl && hl->L[hl->nl - 1].dz) gstore(hl->L[hl->nl - 1].dz + o, dls);
+      if (Gm && hm->L[hm->nl - 1].dz) gstore(hm->L[hm->nl - 1].dz + o, dmu);
+      if (Gl && hl->L[hl->nl - 1].dz) gstore(hl->L[hl->nl - 1].dz + o, dls);
     }
-    Gm[r * LDH + k] = dmu;
+    if (Gm) Gm[r * LDH + k] = dmu;
     if (Gl) Gl[r * LDH + k] = dls;
   }
-  wave_loss_add(lc, ch.loss + 1);
+  if (add_loss) wg_loss_partial(lc, ch.loss_part + 2 * tiles + row0 / FW_ROWS);
 }
 
 // the fit's upstream, read in place from the kernarg segment (see CriticHeadK)
@@ -698,10 +709,10 @@ __device__ __forceinline__ void actor_cc_upstream(ActorHeadK& h, int side, const
       gm = k == bi ? g : 0.f;
       gs = k == bi ? gl : 0.f;
       const size_t o = (size_t)i * C + k;
-      if (hm.L[hm.nl - 1].dz) gstore(hm.L[hm.nl - 1].dz + o, gm);
-      if (hl && hl->L[hl->nl - 1].dz) gstore(hl->L[hl->nl - 1].dz + o, gs);
+      if (Gm && hm.L[hm.nl - 1].dz) gstore(hm.L[hm.nl - 1].dz + o, gm);
+      if (Gl && hl->L[hl->nl - 1].dz) gstore(hl->L[hl->nl - 1].dz + o, gs);
     }
-    Gm[r * LDH + k] = gm;
+    if (Gm) Gm[r * LDH + k] = gm;
     if (Gl) Gl[r * LDH + k] = gs;
   }
 }
@@ -745,7 +756,7 @@ __device__ __forceinline__ void squash_upstream(ActorHeadK& h, int side, const d
     }
     G[r * LDH + k] = gv;
   }
-  if (side == 0 && h.alpha_sum) wave_loss_add(asum, h.alpha_sum);
+  if (side == 0 && h.alpha_sum) wg_loss_partial(asum, h.alpha_sum + row0 / FW_ROWS);
 }
 
 // upstream families compiled into a backward kernel instantiation (each launch kind
@@ -771,7 +782,7 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
     if (eu) { ens_upstream(*eu, h1, h2, G, bA, bB, DT, z, row0 / FW_ROWS, row0, nrows); done = true; }
   }
   if constexpr ((UPF & UPF_CRITIC) != 0) {
-    if (ch) { cert_upstream(*ch, h1, &h2, G, bA, row0, nrows); done = true; }
+    if (ch) { cert_upstream(*ch, &h1, &h2, G, bA, row0, nrows, true); done = true; }
   }
   if constexpr ((UPF & UPF_ACTOR) != 0) {
     if (ah) { actor_cc_upstream(*ah, a.upstream == DRPO_UPSTREAM_SAFE_CC, h1, &h2, G, bA, row0, nrows); done = true; }
@@ -888,7 +899,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
         }
         G[r * LDH + k] = g;
       }
-      wave_loss_add(lq, hq->loss);
+      wg_loss_partial(lq, hq->loss_part + (size_t)sel * ((hq->B + FW_ROWS - 1) / FW_ROWS) + row0 / FW_ROWS);
       lds_barrier();
     } else if (ah && a.upstream == DRPO_UPSTREAM_NEG_MEAN) {
       // the actor loss's -mean(Q_k) (src/ssac.py:472): dL/dQ = -1/B
@@ -928,11 +939,15 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
   for (int e = tid; e < FW_ROWS * twpad; e += FW_NT) DT[(e / twpad) * LDH + e % twpad] = 0.f;
   lds_barrier();
   for (int h = 1; h < a.nnets; ++h) {
-    if (hc && h == 1) {      // vanilla certificate: the mean head only (src/ssac.py:426-435)
-      cert_upstream(*hc, a.net[1], nullptr, G, nullptr, row0, nrows);
+    // generic trunk path (unpaired head shapes): one head at a time, head 1 = mean,
+    // head 2 = log-std (distributional); the certificate loss is added once
+    if (hc) {
+      cert_upstream(*hc, &a.net[1], a.nnets > 2 ? &a.net[2] : nullptr, h == 1 ? G : nullptr, h == 2 ? G : nullptr,
+                    row0, nrows, h == 1);
       lds_barrier();
-    } else if (ha && h == 1) {   // vanilla: the mean head only
-      actor_cc_upstream(*ha, a.upstream == DRPO_UPSTREAM_SAFE_CC, a.net[1], nullptr, G, nullptr, row0, nrows);
+    } else if (ha) {
+      actor_cc_upstream(*ha, a.upstream == DRPO_UPSTREAM_SAFE_CC, a.net[1], a.nnets > 2 ? &a.net[2] : nullptr,
+                        h == 1 ? G : nullptr, h == 2 ? G : nullptr, row0, nrows);
       lds_barrier();
     } else {
       load_gout(a.net[h], G);
@@ -1102,8 +1117,9 @@ static int bwd_multi_launch(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_
     m.actor = *actor;
   }
   if (head) {
-    DRPO_REQUIRE(head->C >= 1 && head->B >= 0 && head->loss && head->log_alpha && head->q0 && head->q1 && head->mu,
-                 "drpo_mlp_backward_multi_head: bad critic head");
+    DRPO_REQUIRE(head->C >= 1 && head->B >= 0 && head->loss_part && head->log_alpha && head->q0 && head->q1 &&
+                     head->mu,
+                 "drpo_mlp_backward_multi_head: bad critic head (loss_part required)");
     m.has_head = 1;
     m.head = *head;
   }

@@ -358,7 +358,9 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   const float coef = S.partial ? s_coef : 1.f;
   if (!live) return;
   if (S.grad_from_sum) {   // a scalar's gradient from a device loss sum (see drpo_optim_seg_t)
-    const float gs = *S.grad_from_sum * (1.f / (float)S.grad_sum_rows);
+    float sum = 0.f;
+    for (int j = 0; j < (S.grad_sum_n > 1 ? S.grad_sum_n : 1); ++j) sum += S.grad_from_sum[j];
+    const float gs = sum * (1.f / (float)S.grad_sum_rows);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float c = S.grad_from_sum_kind == 1 ? 1.f / (1.f + expf(-p[e])) : (S.grad_from_sum_kind == 2 ? 1.f : expf(p[e]));

@@ -51,6 +51,8 @@ struct WgradPlan {
   int64_t slab_off;        // first slab float of the item (tiles with nch > 1)
 };
 
+constexpr int WG_MAXSUMS = 4;
+
 struct WgradArgs {
   drpo_wgrad_item_t it[WG_MAXITEMS];
   WgradPlan pl[WG_MAXITEMS];
@@ -58,9 +60,30 @@ struct WgradArgs {
   int n;
   int has_red;
   drpo_ens_reduce_t red;
+  int nsums;                         // > 0: one extra (logically last) block adds partial sums
+  drpo_sum_t sums[WG_MAXSUMS];
   float* slab;
   unsigned* ctr;
 };
+
+// *out = part[0] + ... + part[n-1] for every entry, in a fixed order (256 strided
+// lanes, then a fixed tree): deterministic, no float atomics
+__device__ __forceinline__ void sums_block(const WgradArgs& a) {
+  __shared__ float red[WG_NT];
+  for (int q = 0; q < a.nsums; ++q) {
+    const drpo_sum_t& S = a.sums[q];
+    float v = 0.f;
+    for (int j = threadIdx.x; j < S.n; j += WG_NT) v += S.part[j];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = WG_NT / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *S.out = red[0];
+    __syncthreads();
+  }
+}
 
 // write-through (sc1) float store / load: the slab hand-off between workgroups
 __device__ __forceinline__ void st_sc1(float* p, float v) {
@@ -334,8 +357,9 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs a) {
   // that each XCD runs one contiguous range: the units of one row chunk (which read the
   // same dZ / Y rows) share an L2
   const int64_t bid = xcd_block().x;
-  if (a.has_red && bid == a.units) {
-    ens_loss_reduce_block(a.red);
+  if (bid >= a.units) {        // the extra blocks: deferred reductions
+    if (a.has_red && bid == a.units) ens_loss_reduce_block(a.red);
+    else if (a.nsums) sums_block(a);
     return;
   }
   int q = 0;
@@ -476,9 +500,25 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, void* workspa
   return drpo_mlp_wgrad_reduce(items, n, nullptr, workspace, workspace_bytes, stream);
 }
 
+static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, const drpo_sum_t* sums,
+                        int nsums, void* workspace, size_t workspace_bytes, hipStream_t stream);
+
 DRPO_API int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red,
                                    void* workspace, size_t workspace_bytes, drpo_stream_t stream_) {
-  hipStream_t stream = (hipStream_t)stream_;
+  return wgrad_launch(items, n, red, nullptr, 0, workspace, workspace_bytes, (hipStream_t)stream_);
+}
+
+DRPO_API int drpo_mlp_wgrad_sums(const drpo_wgrad_item_t* items, int n, const drpo_sum_t* sums, int nsums,
+                                 void* workspace, size_t workspace_bytes, drpo_stream_t stream_) {
+  DRPO_REQUIRE(nsums >= 0 && nsums <= WG_MAXSUMS && (nsums == 0 || sums), "drpo_mlp_wgrad_sums: 0..%d sums",
+               WG_MAXSUMS);
+  for (int q = 0; q < nsums; ++q)
+    DRPO_REQUIRE(sums[q].n >= 0 && sums[q].out && (sums[q].n == 0 || sums[q].part), "drpo_mlp_wgrad_sums: sum %d", q);
+  return wgrad_launch(items, n, nullptr, sums, nsums, workspace, workspace_bytes, (hipStream_t)stream_);
+}
+
+static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, const drpo_sum_t* sums,
+                        int nsums, void* workspace, size_t workspace_bytes, hipStream_t stream) {
   DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS && (n == 0 || items), "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
   static Plan p;   // host scratch (the library is driven by one host thread per process)
   const int rc = plan(items, n, red, p);
@@ -488,7 +528,9 @@ DRPO_API int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items, int n, const 
                "drpo_mlp_wgrad: workspace %zu bytes < %zu (drpo_mlp_wgrad_workspace_size)", workspace_bytes, need);
   p.a.ctr = (unsigned*)workspace;
   p.a.slab = (float*)((char*)workspace + (size_t)((p.tiles * 4 + 255) / 256 * 256));
-  const int64_t blocks = p.a.units + (red ? 1 : 0);
+  p.a.nsums = nsums;
+  for (int q = 0; q < nsums; ++q) p.a.sums[q] = sums[q];
+  const int64_t blocks = p.a.units + (red ? 1 : 0) + (nsums ? 1 : 0);
   if (blocks == 0) return DRPO_OK;
   mlp_wgrad_kernel<<<(unsigned)blocks, WG_NT, wgrad_lds(), stream>>>(p.a);
   DRPO_LAUNCH_CHECK("mlp_wgrad");

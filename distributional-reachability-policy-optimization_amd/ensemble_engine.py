@@ -376,8 +376,11 @@ class EnsembleEngine:
                                            bound=sh is None or sh.rank == 0)
         bd, wl = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
         # the NLL loss rides in the backward launch (its output gradients formed in-kernel)
-        # and its reduction in the weight-gradient launch: forward, backward, wgrad, Adam
-        bd.upstream = 3   # DRPO_UPSTREAM_ENS
+        # and its reduction in the weight-gradient launch: forward, backward, wgrad, Adam.
+        # That needs the paired-heads backward (200- or 256-wide heads, the reference
+        # default); other widths keep the separate loss launch.
+        fused = m.hidden_dim in (200, 256) and S1 <= 64
+        bd.upstream = 3 if fused else 0   # DRPO_UPSTREAM_ENS
         up = EnsUpstream()
         up.D, up.LVR = nets[1].sy[-1].data_ptr(), nets[2].sy[-1].data_ptr()
         up.s_zstride, up.t_zstride, up.b, up.S, up.Z = b * S, b * S1, b, S, Z
@@ -421,8 +424,14 @@ class EnsembleEngine:
             up.s, up.t = fd.src[0], ct.data_ptr() + 4 * k * rows * S1
             red_in.loss = loss_base + 4 * i
             _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
-            _lib.check(L.drpo_mlp_backward_ens(ctypes.byref(bd), ctypes.byref(up), ctypes.byref(red_in),
-                                               ctypes.byref(red), stream), 'ensemble backward')
+            if fused:
+                _lib.check(L.drpo_mlp_backward_ens(ctypes.byref(bd), ctypes.byref(up), ctypes.byref(red_in),
+                                                   ctypes.byref(red), stream), 'ensemble backward')
+            else:
+                largs[2], largs[4], largs[14] = ctypes.c_void_p(up.s), ctypes.c_void_p(up.t), \
+                    ctypes.c_void_p(red_in.loss)
+                _lib.check(L.drpo_ens_loss_partials(*largs, ctypes.byref(red), stream), 'ens_loss')
+                _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
             # the loss reduction rides as the last workgroup of the wgrad launch
             self._wgrad('fit', wl, red, stream)
             if sh is None:

@@ -71,7 +71,8 @@ class Adam:
         """drpo_optim_seg_t for elements [start, end) of this optimizer's tensor:
         clip = (partials, max_norm); ema = (target flat tensor, rate); pack_map = device
         drpo_pack_map_t of the group (refreshes its packed mirrors); grad_from_sum =
-        (device scalar sum, rows): gradient -c(p) * sum / rows of a scalar parameter, with
+        (device sum, rows[, n]): gradient -c(p) * sum / rows of a scalar parameter (the sum
+        of n device partials, added in order), with
         c = exp(p) (kind 0: the SAC temperature), sigmoid(p) (kind 1: the scalar
         multiplier's softplus) or 1 (kind 2: the log-alpha loss);
         grad_scale: multiplier of the gradient (and of its clip norm) -- 1/G after a
@@ -95,6 +96,7 @@ class Adam:
         if grad_from_sum is not None:
             sg.grad_from_sum, sg.grad_sum_rows = grad_from_sum[0].data_ptr(), int(grad_from_sum[1])
             sg.grad_from_sum_kind = int(grad_from_sum_kind)
+            sg.grad_sum_n = int(grad_from_sum[2]) if len(grad_from_sum) > 2 else 1
         sg.grad_scale = float(grad_scale)
         return sg
 

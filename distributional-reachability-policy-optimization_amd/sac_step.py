@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._abi import (ActorHead, BufferView, CriticHead, MlpBwd, MlpFwd, WgradItem)
+from ._abi import (ActorHead, BufferView, CriticHead, MlpBwd, MlpFwd, SumDesc, WgradItem)
 from .optim import ema_segment, fused_step, grad_sumsq_multi
 
 ACT_ID = {None: 0, 'identity': 0, 'relu': 1, 'swish': 2, 'tanh': 3}
@@ -247,12 +247,10 @@ class SACEngine:
         # the actor's and the safe actor's flat gradients and the alpha-loss sum are
         # adjacent slices of one arena (the critic and multiplier phases already exchange
         # one flat buffer each).
-        ga, gs = solver.actor.group, solver.actor_safe.group
-        na, ns = ga.size, gs.size
-        self.actor_xchg = torch.zeros(na + ns + 64, device=self.dev)
-        ga.move_grad(self.actor_xchg[:na], solver.actor)
-        gs.move_grad(self.actor_xchg[na:na + ns], solver.actor_safe)
-        self.alpha_sum = self.actor_xchg[na + ns:na + ns + 1]   # zeroed by the step that consumes it
+        # the alpha-loss sum travels as its per-16-row-tile partials (written, not
+        # accumulated, by the squash backward; summed in order by the optimizer launch)
+        self.actor_xchg = None
+        self._actor_arena(solver.batch_size)
         self.loss_pool = None
         self.loss_pos = 0
         self._zeroed = set()   # groups whose grads the last fused step left zeroed
@@ -274,10 +272,27 @@ class SACEngine:
         self.loss_pos += n
         return s
 
+    def _actor_arena(self, B):
+        """(Re)build the actor exchange arena for batch B: actor grads | safe actor grads |
+        one alpha-loss partial per 16-row tile."""
+        nt = (B + 15) // 16
+        if self.actor_xchg is not None and self.alpha_sum.numel() >= nt:
+            return
+        sol = self.sol
+        ga, gs = sol.actor.group, sol.actor_safe.group
+        na, ns = ga.size, gs.size
+        self.actor_xchg = torch.zeros(na + ns + nt, device=self.dev)
+        ga.move_grad(self.actor_xchg[:na], sol.actor)
+        gs.move_grad(self.actor_xchg[na:na + ns], sol.actor_safe)
+        self.alpha_sum = self.actor_xchg[na + ns:]
+        if hasattr(self, 'desc'):
+            self.desc.pop('a.head', None)
+
     def _setup(self, B):
         if self.B == B:
             return
         self.B = B
+        self._actor_arena(B)
         self.ws = {}
         sol, S, A, C = self.sol, self.S, self.A, self.C
         cg, tg = sol.critic_group, sol.critic_target_group
@@ -401,16 +416,24 @@ class SACEngine:
         if ev:
             self.profiler.end(ev)
 
-    def _run_wgrad(self, key, builder):
-        """One grouped weight-gradient launch; returns the clip-partial slots per segment."""
+    def _run_wgrad(self, key, builder, sums=None):
+        """One grouped weight-gradient launch; returns the clip-partial slots per segment.
+        sums: [(partials, out)] -- loss partials the launch's extra block adds up in order
+        into the 0-d `out` (drpo_mlp_wgrad_sums)."""
         d = self.desc.get(key)
         if d is None:
             arr, n, used = builder()
             ws = wgrad_workspace(self.wg_ws, key, arr, n, self.dev)
-            d = self.desc[key] = (arr, n, used, ws)
-        arr, n, used, ws = d
+            d = self.desc[key] = (arr, n, used, ws, (SumDesc * 4)())
+        arr, n, used, ws, sd = d
         ev = self.profiler.begin('mlp_wgrad', key, wgrad_flops(arr, n)) if self.profiler else None
-        _lib.check(_lib.lib().drpo_mlp_wgrad(arr, n, ws.data_ptr(), ws.numel(), _lib.stream()), key)
+        if sums:
+            for q, (part, out) in enumerate(sums):
+                sd[q].part, sd[q].n, sd[q].out = part.data_ptr(), part.numel(), out.data_ptr()
+            _lib.check(_lib.lib().drpo_mlp_wgrad_sums(arr, n, sd, len(sums), ws.data_ptr(), ws.numel(),
+                                                      _lib.stream()), key)
+        else:
+            _lib.check(_lib.lib().drpo_mlp_wgrad(arr, n, ws.data_ptr(), ws.numel(), _lib.stream()), key)
         if ev:
             self.profiler.end(ev)
         return used
@@ -552,6 +575,11 @@ class SACEngine:
         ch.dc = ws['c.dm'].data_ptr() if robust else 0
         ch.seed, ch.ctr = noise.seed, ctr
         ch.loss = loss.data_ptr()
+        # per-16-row-tile loss partials (twin 0 | twin 1 | certificate), summed into
+        # loss[0] / loss[1] by the weight-gradient launch's extra block
+        nt = (B + 15) // 16
+        lpart = self.buf('c.lpart', 3 * nt)
+        ch.loss_part = lpart.data_ptr()
         # backward: critics (twin) and constraint critic (trunk + heads), each job forming
         # its own output gradients (and loss) from the critic head in-kernel
         # (src/ssac.py:284-456: compute_target, compute_cons_target, both losses)
@@ -565,7 +593,8 @@ class SACEngine:
         if dist:
             items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]], 'cc'))
         sq = self._sq('c', ('c', 'cc'))
-        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq))
+        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq),
+                               sums=[(lpart[:2 * nt], loss[0]), (lpart[2 * nt:], loss[1])])
         cg = sol.critic_group
         self.dp.sum_(cg.grad)      # the 1/G of the mean rides in the optimizer segments
         crange = cg.span('critic.')
@@ -717,9 +746,10 @@ class SACEngine:
         # its "i == 2" clip / schedule of the safe actor never fires (src/ssac.py:507-527)
         safe_full = sol.autotune_alpha
         if sol.autotune_alpha:
-            # the gradient is formed from the sum; zero_grad clears the sum slot for the next step
-            segs.append(aopt.segment(0, 1, aopt.step_scalars(), grad=asum, grad_from_sum=(asum, B * self.dp.world),
-                                     grad_from_sum_kind=2 if sol.use_log_alpha_loss else 0, zero_grad=True))
+            # the gradient is formed from the summed tile partials (overwritten each step)
+            segs.append(aopt.segment(0, 1, aopt.step_scalars(), grad=asum[:1],
+                                     grad_from_sum=(asum, B * self.dp.world, (B + 15) // 16),
+                                     grad_from_sum_kind=2 if sol.use_log_alpha_loss else 0))
         segs.append(sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
                                                      clip=(ps, sol.grad_norm) if safe_full else None, zero_grad=True,
                                                      pack_map=gs.pack_map(), grad_scale=gsc))

@@ -228,7 +228,8 @@ typedef struct {
   const float* logp;            /* actor log-probs [B] */
   const float* log_alpha;       /* the actor's log-prob terms scaled by exp(*log_alpha) * lp_scale; NULL: none */
   float lp_scale, target_entropy;
-  float* alpha_sum;             /* += sum(logp + target_entropy) (actor), or NULL */
+  float* alpha_sum;             /* per row tile: sum(logp + target_entropy) of the actor's rows, or NULL
+                                   (one float per 16-row tile, overwritten; drpo_optim_seg_t.grad_sum_n) */
 } drpo_actor_head_t;
 
 /* drpo_mlp_bwd_t.upstream */
@@ -291,6 +292,9 @@ typedef struct {
   const float *mu, *ls;
   float *dq0, *dq1, *dmu, *dls;
   float* loss; /* [2] accumulated: critic loss, constraint-critic loss */
+  float* loss_part;   /* drpo_mlp_backward_multi_head only: per-workgroup loss partials instead of
+                         atomics into loss: [3][row tiles] = twin 0, twin 1, certificate (summed by
+                         a drpo_mlp_wgrad_sums reduction) */
 } drpo_critic_head_t;
 
 int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);
@@ -334,6 +338,16 @@ int drpo_mlp_wgrad(const drpo_wgrad_item_t* items /* host */, int n, void* works
  * reduction (drpo_ens_loss_partials); red may be NULL */
 int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items /* host */, int n, const drpo_ens_reduce_t* red /* host */,
                           void* workspace, size_t workspace_bytes, drpo_stream_t stream);
+/* drpo_mlp_wgrad plus one extra workgroup adding up partial sums in a fixed order:
+ * *out = part[0] + part[1] + ... + part[n-1] for each of nsums (<= 4) entries (the
+ * per-workgroup loss partials of drpo_mlp_backward_multi_head; no float atomics) */
+typedef struct {
+  const float* part;
+  int n;
+  float* out;
+} drpo_sum_t;
+int drpo_mlp_wgrad_sums(const drpo_wgrad_item_t* items /* host */, int n, const drpo_sum_t* sums /* host */,
+                        int nsums, void* workspace, size_t workspace_bytes, drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- packed weight mirrors
  * Every MLP kernel streams weights from fragment-linear mirrors of the PyTorch
@@ -503,6 +517,7 @@ typedef struct {
                                  norm is that of the scaled gradient): 1/G folds the data-
                                  parallel mean into the step after a SUM all-reduce. 0 is
                                  read as 1, so zero-initialised descriptors keep plain grads */
+  int grad_sum_n;             /* grad_from_sum holds this many partial sums, added in order (0 = 1) */
 } drpo_optim_seg_t;
 
 int drpo_optim_step(const drpo_optim_seg_t* segs /* host, <= 8 */, int n, drpo_stream_t stream);
