@@ -353,14 +353,22 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
       s_coef = c < 1.f ? c : 1.f;
     }
   }
-  if (S.map || S.partial) __syncthreads();
+  // a scalar's gradient from device loss partials: the first wave adds them (lane-strided,
+  // then a fixed shuffle tree: deterministic), instead of one thread walking the list
+  __shared__ float s_gsum;
+  if (S.grad_from_sum && threadIdx.x < 64) {
+    const int ns = S.grad_sum_n > 1 ? S.grad_sum_n : 1;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < ns; i += 64) s += S.grad_from_sum[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (threadIdx.x == 0) s_gsum = s;
+  }
+  if (S.map || S.partial || S.grad_from_sum) __syncthreads();
   const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
   const float coef = S.partial ? s_coef : 1.f;
   if (!live) return;
   if (S.grad_from_sum) {   // a scalar's gradient from a device loss sum (see drpo_optim_seg_t)
-    float sum = 0.f;
-    for (int j = 0; j < (S.grad_sum_n > 1 ? S.grad_sum_n : 1); ++j) sum += S.grad_from_sum[j];
-    const float gs = sum * (1.f / (float)S.grad_sum_rows);
+    const float gs = s_gsum * (1.f / (float)S.grad_sum_rows);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float c = S.grad_from_sum_kind == 1 ? 1.f / (1.f + expf(-p[e])) : (S.grad_from_sum_kind == 2 ? 1.f : expf(p[e]));

@@ -35,11 +35,39 @@ using namespace drpo;
 namespace {
 constexpr int WG_NW = 4;                 // waves per workgroup
 constexpr int WG_NT = WG_NW * 64;
-constexpr int WG_D = 5;                  // register ring slots (k-groups of 4 rows each)
+#ifndef DRPO_WG_D
+#define DRPO_WG_D 5
+#endif
+constexpr int WG_D = DRPO_WG_D;          // register ring slots (k-groups of 4 rows each; A/B macro)
 constexpr int WG_ROWQ = 64;              // chunk granularity (rows)
 constexpr int WG_MAXITEMS = 16;
 constexpr int WG_SLD = 264;              // LDS slab stride per accumulator block (== 8 mod 32)
 }  // namespace
+
+#ifdef DRPO_STAMPS
+// profiling builds only (profiles/wgrad_probe.py): per-workgroup s_memtime stamps
+__device__ unsigned long long g_stamps_wg[1 << 14][8];
+#define STAMPG(i)                                                                                 \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long _t;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) g_stamps_wg[blockIdx.x][(i)] = _t;           \
+  } while (0)
+DRPO_API int drpo_debug_stamps_wgrad(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_wg), sizeof(unsigned long long) * 8 * (size_t)n);
+}
+DRPO_API int drpo_debug_stamps_wgrad_clear() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps_wg)) != hipSuccess) return 1;
+  return (int)hipMemset(p, 0, sizeof(g_stamps_wg));
+}
+#else
+#define STAMPG(i) \
+  do {            \
+  } while (0)
+#endif
 
 struct WgradPlan {
   int to, ti;              // tile shape (64 or 16)
@@ -68,8 +96,7 @@ struct WgradArgs {
 
 // *out = part[0] + ... + part[n-1] for every entry, in a fixed order (256 strided
 // lanes, then a fixed tree): deterministic, no float atomics
-__device__ __forceinline__ void sums_block(const WgradArgs& a) {
-  __shared__ float red[WG_NT];
+__device__ __forceinline__ void sums_block(const WgradArgs& a, float* red) {
   for (int q = 0; q < a.nsums; ++q) {
     const drpo_sum_t& S = a.sums[q];
     float v = 0.f;
@@ -231,8 +258,12 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
       __builtin_amdgcn_sched_barrier(0);
       if (s0 + v >= WG_D - 1) use(s0 + v - (WG_D - 1), ra[(v + 1) % WG_D], rb[(v + 1) % WG_D]);
     }
+#ifdef DRPO_STAMPS
+    if (s0 == WG_D) STAMPG(5);   // the first k-group consumed: the ring's fill latency
+#endif
   }
 
+  STAMPG(1);
   // the 4 waves' partial tiles -> LDS slabs (conflict-free: lanes write consecutive words)
   float* R = lds;
 #pragma unroll
@@ -277,6 +308,7 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
 #pragma unroll
     for (int w = 0; w < WG_NW; ++w) pb += Rb[w * TO + tid];
   }
+  STAMPG(2);
   constexpr int SL = TO * TI + TO;            // slab floats per unit (tile + bias)
   float* gW = I.gW + (size_t)zb * I.gwstride;
   float* gb = I.gb + (size_t)zb * I.gbstride;
@@ -297,6 +329,7 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
       s_last = last;
     }
     __syncthreads();
+    STAMPG(3);
     if (!s_last) return;
     // last arriver: the tile's partials in chunk order
     const float* base = a.slab + P.slab_off + tile_local * P.nch * SL;
@@ -340,6 +373,7 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
     const float s = wg_block_sum(sq, red);
     if (tid == 0) I.sq[I.sq_off + tile_local] = s;
   }
+  STAMPG(4);
 }
 
 template <int TO, int TI>
@@ -356,10 +390,11 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs a) {
   // logical order: item, then (member, chunk, o-tile, i-tile) with i fastest, spread so
   // that each XCD runs one contiguous range: the units of one row chunk (which read the
   // same dZ / Y rows) share an L2
+  STAMPG(0);
   const int64_t bid = xcd_block().x;
   if (bid >= a.units) {        // the extra blocks: deferred reductions
     if (a.has_red && bid == a.units) ens_loss_reduce_block(a.red);
-    else if (a.nsums) sums_block(a);
+    else if (a.nsums) sums_block(a, wsm);
     return;
   }
   int q = 0;
@@ -424,7 +459,12 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
   }
   a.n = m;
   // chunk sizes: every unit about the same cost, all units resident at once (<= 2 per CU)
-  const int64_t slots = 2 * (int64_t)wg_cus();
+  static const int per_cu = [] {   // A/B knob (profiles/wgrad_probe.py)
+    const char* e = getenv("DRPO_WGRAD_PER_CU");
+    const int v = e ? atoi(e) : 2;
+    return v >= 1 && v <= 64 ? v : 2;
+  }();
+  const int64_t slots = per_cu * (int64_t)wg_cus();
   auto units_for = [&](double per, int* nch, int* chunk) {
     int64_t tot = 0;
     for (int k = 0; k < m; ++k) {
