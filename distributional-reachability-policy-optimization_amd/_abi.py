@@ -49,7 +49,7 @@ class OptimSeg(ctypes.Structure):
                 ('eps', c_float), ('weight_decay', c_float), ('zero_grad', c_int),
                 ('ema_target', P), ('ema_rate', c_float), ('ema_keep', c_float), ('map', P),
                 ('grad_from_sum', P), ('grad_sum_rows', c_int64), ('grad_from_sum_kind', c_int),
-                ('grad_scale', c_float), ('grad_sum_n', c_int)]
+                ('grad_scale', c_float), ('grad_sum_n', c_int), ('map_host', P)]
 
 
 class EnsReduce(ctypes.Structure):

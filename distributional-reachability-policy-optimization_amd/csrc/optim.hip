@@ -8,6 +8,8 @@
 //   drpo_ema         : target <- rate*p + (1-rate)*target (src/torch_util.py:223-226)
 //   drpo_normalizer_fit : column mean / unbiased std over the replay states
 //                      (src/normalization.py:14-19)
+#include <algorithm>
+
 #include "common.hpp"
 
 using namespace drpo;
@@ -218,25 +220,44 @@ DRPO_API int drpo_normalize(const float* x, const float* mean, const float* std,
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int OPT_MAXSEG = 8;
-constexpr int OPT_BLOCK_ELEMS = 1024;   // elements per workgroup (256 threads x 4)
+constexpr int OPT_MAXTASK = 32;
+constexpr int OPT_BLOCK_ELEMS = 1024;   // flat task: elements per workgroup (256 threads x 4)
+constexpr int OPT_BLOCKS4 = 64;         // matrix task: 4x4 blocks per workgroup (one per lane quad)
 }
 
-struct OptimArgs {
-  drpo_optim_seg_t seg[OPT_MAXSEG];
-  int64_t first[OPT_MAXSEG + 1];        // block prefix per segment
-  int n;
+// A launch is a list of tasks, each a run of workgroups over one segment:
+//  * flat: elements [a, b), 4 consecutive per thread (biases, scalars, anything
+//    outside a weight matrix, and matrices of segments without a host map);
+//  * matrix: whole members [z0, z0 + nz) of one [nbatch][dout][din] weight matrix,
+//    one 4x4 block (4 rows x 4 columns) per lane quad. Every access is then a 16-byte
+//    row segment: the flat group's p / g / m / v / EMA target rows, the forward
+//    mirror (a fragment lane holds 4 consecutive columns of one row) and the
+//    transposed mirror (a fragment lane holds 4 consecutive rows of one column) --
+//    where the flat form issued 4 scattered 4-byte transposed-mirror stores per
+//    thread (round 3 probe: 13.8 us -> 7.6 us per fit step without the mirror stores).
+struct OptTask {
+  int64_t a, b;                         // flat: element range; matrix: flat offset of member 0, blocks
+  int seg, kind;                        // kind 0 flat, 1 matrix (din % 4 == 0), 2 matrix (scalar rows)
+  int layer, din, dout, z0;             // matrix: its entry in the segment's (device) pack map
+  int map_needed;                       // flat: the range overlaps a weight matrix
 };
+
+struct OptimArgs {
+  int64_t first[OPT_MAXTASK];           // first workgroup of each task (unused slots: INT64_MAX)
+  OptTask task[OPT_MAXTASK];
+  drpo_optim_seg_t seg[OPT_MAXSEG];
+  int ntask;
+};
+static_assert(sizeof(OptimArgs) <= 4096, "optimizer kernarg");
 
 // Packed-mirror refresh for the n (<= 4) consecutive flat elements i0.. of one thread.
 // The weight matrix holding i0 is found once; the (member, row, column) coordinates
 // are divided out once and then stepped (consecutive elements are consecutive
 // columns), so the per-element cost is a few integer adds instead of two 32-bit
-// divisions and a layer search.
+// divisions and a layer search. (Flat tasks only: segments without a host map, or
+// partial members of a matrix.)
 __device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i0, int n, const float (&pv)[4],
                                             const float (&tv)[4], bool has_t) {
-  // Every tensor of a flat group starts 64-float aligned (params.py) and i0 is a
-  // multiple of 4 whenever n > 1, so the n elements never reach into a second weight
-  // matrix: past the end of the one holding i0 lies bias or padding.
   const int nl = mp->nlayers;
   int l = 0;
   int64_t rel64 = 0;
@@ -255,23 +276,6 @@ __device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i
   float* P = mp->P;
   float* Pt = has_t ? mp->Pt : nullptr;
   float* PT = mp->PT;
-  if (n == 4 && (din & 3) == 0) {
-    // k is a multiple of 4 and k..k+3 stay in row o: the 4 forward-mirror components
-    // of one fragment lane are contiguous (one 16-byte store)
-    const int64_t base = mp->poff[l] + (int64_t)z * ncb * nks * 256;
-    const int64_t pi = base + ((int64_t)((o >> 4) * nks + (k >> 4)) << 8) + ((((k >> 2) & 3) * 16 + (o & 15)) << 2);
-    if (P) *reinterpret_cast<f32x4*>(P + pi) = f32x4{pv[0], pv[1], pv[2], pv[3]};
-    if (Pt) *reinterpret_cast<f32x4*>(Pt + pi) = f32x4{tv[0], tv[1], tv[2], tv[3]};
-    if (PT) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kk = k + e;
-        const int64_t ti = base + ((int64_t)((kk >> 4) * ncb + (o >> 4)) << 8) + ((((o >> 2) & 3) * 16 + (kk & 15)) << 2) + (o & 3);
-        PT[ti] = pv[e];
-      }
-    }
-    return;
-  }
   for (int e = 0; e < n; ++e) {
     const int64_t base = mp->poff[l] + (int64_t)z * ncb * nks * 256;
     // forward mirror: fragment (o>>4, k>>4), lane ((k>>2)&3)*16 + (o&15), component k&3
@@ -292,25 +296,158 @@ __device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i
   }
 }
 
+// per-element update shared by both task kinds: g (already scaled) -> Adam on p, m, v
+__device__ __forceinline__ void adam_elem(const drpo_optim_seg_t& S, float coef, float g, float& p, float& m,
+                                          float& v) {
+  float ge = g * coef;
+  if (S.weight_decay != 0.f) ge = fmaf(p, S.weight_decay, ge);
+  m = torch_lerp(m, ge, 1.f - S.beta1);
+  v = fmaf(v, S.beta2, (1.f - S.beta2) * ge * ge);
+  const float denom = sqrtf(v) / S.bc2_sqrt + S.eps;
+  p = p - S.lr_over_bc1 * (m / denom);
+}
+
+// EMA of one target element (one explicit fma: both task kinds round alike)
+__device__ __forceinline__ float ema_elem(const drpo_optim_seg_t& S, float p, float t) {
+  return fmaf(S.ema_rate, p, S.ema_keep * t);
+}
+
+// x[i] for a per-lane i, by bit masks (a select chain is turned back into an indexed
+// private array, i.e. scratch memory)
+__device__ __forceinline__ float pick4(const float (&x)[4], int i) {
+  unsigned r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r |= __float_as_uint(x[k]) & (0u - (unsigned)(i == k));
+  return __uint_as_float(r);
+}
+
+// One 4x4 block of a weight matrix per 4 adjacent lanes: lane rr = tid & 3 owns row
+// o0 + rr, columns k0..k0+3 (masked past dout / din; VEC: din % 4 == 0, so the row
+// segment is one 16-byte access). After the update a 4x4 transpose inside the lane
+// quad (3 xor shuffles) hands lane rr column k0 + rr of rows o0..o0+3: the transposed
+// mirror's 16-byte fragment component group.
+template <bool VEC>
+__device__ __forceinline__ void opt_matrix_block(const drpo_optim_seg_t& S, const OptTask& T, int64_t blk, int rr,
+                                                 bool live, float coef, float gscale) {
+  const int din = T.din, dout = T.dout;
+  const int nkb = (din + 3) >> 2, nob = (dout + 3) >> 2;
+  const int per = nkb * nob;
+  const int64_t zb = blk / per;
+  const int z = T.z0 + (int)zb;
+  const int r = (int)(blk - zb * per);
+  const int ob = r / nkb, kb = r - ob * nkb;
+  const int o0 = 4 * ob, k0 = 4 * kb;
+  const int o = o0 + rr;
+  const bool row = live && o < dout;
+  const int64_t i = T.a + (int64_t)z * din * dout + (int64_t)o * din + k0;
+  float p[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f};
+  float v[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool has_t = S.ema_target != nullptr;
+  auto ld = [&](const float* src, float (&dst)[4]) {
+    if (!row) return;
+    if constexpr (VEC) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(src + i);
+      dst[0] = x[0]; dst[1] = x[1]; dst[2] = x[2]; dst[3] = x[3];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[c] = k0 + c < din ? src[i + c] : 0.f;
+    }
+  };
+  auto st = [&](float* dst, const float (&src)[4]) {
+    if (!row) return;
+    if constexpr (VEC) {
+      *reinterpret_cast<f32x4*>(dst + i) = f32x4{src[0], src[1], src[2], src[3]};
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (k0 + c < din) dst[i + c] = src[c];
+    }
+  };
+  ld(S.p, p);
+  if (S.adam) {
+    ld(S.g, g);
+    ld(S.m, m);
+    ld(S.v, v);
+  }
+  if (has_t) ld(S.ema_target, t);
+  if (S.adam) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) adam_elem(S, coef, g[c] * gscale, p[c], m[c], v[c]);
+    st(S.m, m);
+    st(S.v, v);
+    st(S.p, p);
+  }
+  if (S.zero_grad) {
+    const float zz[4] = {0.f, 0.f, 0.f, 0.f};
+    st(S.g, zz);
+  }
+  if (has_t) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[c] = ema_elem(S, p[c], t[c]);
+    st(S.ema_target, t);
+  }
+  // mirrors (device map, scalar loads). Masked elements are 0, the mirrors' padding value.
+  const drpo_pack_map_t* md = S.map;
+  const int ncb = (dout + 15) >> 4, nks = (din + 15) >> 4;
+  const int64_t mb = md->poff[T.layer] + (int64_t)z * ncb * nks * 256;
+  float* P = md->P;
+  float* PT = md->PT;
+  float* Pt = has_t ? md->Pt : nullptr;
+  // forward mirror: row o's columns k0..k0+3 are the 4 components of fragment
+  // (o>>4, k0>>4), lane ((k0>>2)&3)*16 + (o&15)
+  if (row) {
+    const int64_t pi = mb + ((int64_t)((o >> 4) * nks + (k0 >> 4)) << 8) + ((((k0 >> 2) & 3) * 16 + (o & 15)) << 2);
+    if (P) *reinterpret_cast<f32x4*>(P + pi) = f32x4{p[0], p[1], p[2], p[3]};
+    if (Pt) *reinterpret_cast<f32x4*>(Pt + pi) = f32x4{t[0], t[1], t[2], t[3]};
+  }
+  if (PT) {
+    // quad transpose: q[j] = row o0 + j, column k0 + rr
+    float q[4];
+    q[0] = q[1] = q[2] = q[3] = 0.f;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const float sent = pick4(p, rr ^ x);
+      const float got = x == 0 ? sent : __shfl_xor(sent, x, 64);
+      const unsigned gb = __float_as_uint(got), j = (unsigned)(rr ^ x);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)   // q[j] = got (masks: see pick4)
+        q[c] = __uint_as_float(__float_as_uint(q[c]) | (gb & (0u - (unsigned)(j == (unsigned)c))));
+    }
+    // transposed mirror: column k's rows o0..o0+3 are the 4 components of fragment
+    // (k>>4, o0>>4), lane ((o0>>2)&3)*16 + (k&15)
+    const int k = k0 + rr;
+    if (live && k < din) {
+      const int64_t ti = mb + ((int64_t)((k >> 4) * ncb + (o0 >> 4)) << 8) + ((((o0 >> 2) & 3) * 16 + (k & 15)) << 2);
+      *reinterpret_cast<f32x4*>(PT + ti) = f32x4{q[0], q[1], q[2], q[3]};
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
-  __shared__ float s_coef;
-  // the segment's pack map, staged once per workgroup: the per-thread layer search
-  // of pack_write4 then reads LDS instead of a chain of dependent global loads
+  __shared__ float s_coef, s_gsum;
+  // the segment's pack map (flat tasks overlapping a matrix), staged once per workgroup:
+  // the per-thread layer search of pack_write4 then reads LDS instead of a chain of
+  // dependent global loads
   __shared__ __attribute__((aligned(16))) int s_map[(sizeof(drpo_pack_map_t) + 3) / 4];
   const int64_t bid = blockIdx.x;
-  int q = 0;
-  while (q + 1 < a.n && bid >= a.first[q + 1]) ++q;
-  const drpo_optim_seg_t& S = a.seg[q];
-  const int64_t e0 = S.start + (bid - a.first[q]) * OPT_BLOCK_ELEMS;
-  const int64_t e1 = min(S.end, e0 + OPT_BLOCK_ELEMS);
-  // Each thread owns 4 consecutive elements. Its element loads are issued FIRST, so
+  // the task: the number of prefixes <= bid. All prefixes are read at once (independent
+  // scalar loads, one kernarg round trip) instead of a chain of dependent ones.
+  int lo = -1;
+#pragma unroll
+  for (int i = 0; i < OPT_MAXTASK; ++i) lo += bid >= a.first[i] ? 1 : 0;
+  const OptTask& T = a.task[lo];
+  const drpo_optim_seg_t& S = a.seg[T.seg];
+  const int64_t lb = bid - a.first[lo];
+  const bool matrix = T.kind != 0;
+  // Flat: each thread owns 4 consecutive elements, whose loads are issued FIRST, so
   // they are in flight together with the pack-map staging and the clip partial sums
-  // (one memory latency per workgroup instead of three in a row: the element loads
-  // depend on neither).
+  // (one memory latency per workgroup instead of three in a row).
+  const int64_t e0 = T.a + lb * OPT_BLOCK_ELEMS;
+  const int64_t e1 = min(T.b, e0 + OPT_BLOCK_ELEMS);
   const int64_t i0 = e0 + 4 * (int64_t)threadIdx.x;
-  const bool live = i0 < e1;
+  const bool live = !matrix && i0 < e1;
   const int n = live ? (int)min((int64_t)4, e1 - i0) : 0;
-  const bool vec = n == 4 && (S.start & 3) == 0;
+  const bool vec = n == 4 && (i0 & 3) == 0;
   float p[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f};
   float v[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
   auto ld4 = [&](const float* src, float (&dst)[4]) {
@@ -337,7 +474,8 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
     }
     if (S.ema_target) ld4(S.ema_target, t);
   }
-  if (S.map) {
+  const bool stage_map = !matrix && S.map && T.map_needed;
+  if (stage_map) {
     const int* src = reinterpret_cast<const int*>(S.map);
     for (int i = threadIdx.x; i < (int)(sizeof(drpo_pack_map_t) / 4); i += 256) s_map[i] = src[i];
   }
@@ -355,7 +493,6 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   }
   // a scalar's gradient from device loss partials: the first wave adds them (lane-strided,
   // then a fixed shuffle tree: deterministic), instead of one thread walking the list
-  __shared__ float s_gsum;
   if (S.grad_from_sum && threadIdx.x < 64) {
     const int ns = S.grad_sum_n > 1 ? S.grad_sum_n : 1;
     float s = 0.f;
@@ -363,9 +500,17 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
     for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
     if (threadIdx.x == 0) s_gsum = s;
   }
-  if (S.map || S.partial || S.grad_from_sum) __syncthreads();
-  const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
+  if (stage_map || S.partial || S.grad_from_sum) __syncthreads();
   const float coef = S.partial ? s_coef : 1.f;
+  if (matrix) {
+    // every lane of a quad takes part in the transpose: out-of-range quads run masked
+    const int64_t blk = lb * OPT_BLOCKS4 + (threadIdx.x >> 2);
+    const bool in = blk < T.b;
+    const int64_t b = in ? blk : T.b - 1;
+    if (T.kind == 1) opt_matrix_block<true>(S, T, b, threadIdx.x & 3, in, coef, gscale);
+    else opt_matrix_block<false>(S, T, b, threadIdx.x & 3, in, coef, gscale);
+    return;
+  }
   if (!live) return;
   if (S.grad_from_sum) {   // a scalar's gradient from a device loss sum (see drpo_optim_seg_t)
     const float gs = s_gsum * (1.f / (float)S.grad_sum_rows);
@@ -380,14 +525,7 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   }
   if (S.adam) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float ge = g[e] * coef;
-      if (S.weight_decay != 0.f) ge = fmaf(p[e], S.weight_decay, ge);
-      m[e] = torch_lerp(m[e], ge, 1.f - S.beta1);
-      v[e] = fmaf(v[e], S.beta2, (1.f - S.beta2) * ge * ge);
-      const float denom = sqrtf(v[e]) / S.bc2_sqrt + S.eps;
-      p[e] = p[e] - S.lr_over_bc1 * (m[e] / denom);
-    }
+    for (int e = 0; e < 4; ++e) adam_elem(S, coef, g[e], p[e], m[e], v[e]);
     st4(S.m, m);
     st4(S.v, v);
     st4(S.p, p);
@@ -398,36 +536,76 @@ __global__ __launch_bounds__(256) void optim_step_kernel(OptimArgs a) {
   }
   if (S.ema_target) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) t[e] = S.ema_rate * p[e] + S.ema_keep * t[e];
+    for (int e = 0; e < 4; ++e) t[e] = ema_elem(S, p[e], t[e]);
     st4(S.ema_target, t);
   }
-  if (S.map) {
-    if (vec) {
-      pack_write4(map, i0, 4, p, t, S.ema_target != nullptr);
-    } else {
-      for (int e = 0; e < n; ++e) {
-        const float pe[4] = {p[e], 0.f, 0.f, 0.f}, te[4] = {t[e], 0.f, 0.f, 0.f};
-        pack_write4(map, i0 + e, 1, pe, te, S.ema_target != nullptr);
-      }
-    }
+  if (stage_map) {
+    const drpo_pack_map_t* map = reinterpret_cast<const drpo_pack_map_t*>(s_map);
+    pack_write4(map, i0, n, p, t, S.ema_target != nullptr);
   }
 }
+
+namespace {
+// task list of one segment: each whole-member run of a weight matrix (from the host
+// map) as a matrix task, the ranges between them as flat tasks
+int plan_segment(const drpo_optim_seg_t& S, int k, OptimArgs& a, int64_t& tot) {
+  auto flat = [&](int64_t x, int64_t y, int needed) {
+    if (y <= x) return DRPO_OK;
+    DRPO_REQUIRE(a.ntask < OPT_MAXTASK, "drpo_optim_step: more than %d tasks", OPT_MAXTASK);
+    OptTask& T = a.task[a.ntask++];
+    T = OptTask{};
+    a.first[a.ntask - 1] = tot;
+    T.a = x; T.b = y; T.seg = k; T.kind = 0; T.map_needed = needed;
+    tot += (y - x + OPT_BLOCK_ELEMS - 1) / OPT_BLOCK_ELEMS;
+    return DRPO_OK;
+  };
+  const drpo_pack_map_t* mh = S.map ? S.map_host : nullptr;
+  if (!mh) return flat(S.start, S.end, S.map != nullptr);
+  // matrices in flat order
+  int order[16], nl = mh->nlayers < 16 ? mh->nlayers : 16;
+  for (int l = 0; l < nl; ++l) order[l] = l;
+  for (int i = 1; i < nl; ++i)
+    for (int j = i; j > 0 && mh->off[order[j]] < mh->off[order[j - 1]]; --j) std::swap(order[j], order[j - 1]);
+  int64_t cur = S.start;
+  for (int q = 0; q < nl; ++q) {
+    const int l = order[q];
+    const int64_t msz = (int64_t)mh->din[l] * mh->dout[l];
+    const int64_t off = mh->off[l], endm = off + msz * mh->nbatch[l];
+    const int64_t x = std::max(off, S.start), y = std::min(endm, S.end);
+    if (y <= x || msz == 0) continue;
+    const int64_t za = (x - off + msz - 1) / msz, zb = (y - off) / msz;   // whole members inside
+    if (za >= zb || a.ntask + 2 > OPT_MAXTASK - 1) continue;   // partial only / list full: flat
+    int rc = flat(cur, off + za * msz, 1);
+    if (rc != DRPO_OK) return rc;
+    OptTask& T = a.task[a.ntask++];
+    T = OptTask{};
+    a.first[a.ntask - 1] = tot;
+    T.seg = k; T.kind = (mh->din[l] & 3) == 0 ? 1 : 2;
+    T.a = off; T.layer = l; T.din = mh->din[l]; T.dout = mh->dout[l]; T.z0 = (int)za;
+    T.b = (zb - za) * (int64_t)((mh->din[l] + 3) / 4) * ((mh->dout[l] + 3) / 4);   // 4x4 blocks
+    tot += (T.b + OPT_BLOCKS4 - 1) / OPT_BLOCKS4;
+    cur = off + zb * msz;
+  }
+  return flat(cur, S.end, 1);
+}
+}  // namespace
 
 DRPO_API int drpo_optim_step(const drpo_optim_seg_t* segs, int n, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(n >= 0 && n <= OPT_MAXSEG, "drpo_optim_step: at most %d segments", OPT_MAXSEG);
-  OptimArgs a{};
+  static OptimArgs a;   // host scratch (the library is driven by one host thread per process)
+  a = OptimArgs{};
+  for (int i = 0; i < OPT_MAXTASK; ++i) a.first[i] = INT64_MAX;
   int64_t tot = 0;
   for (int k = 0; k < n; ++k) {
     const drpo_optim_seg_t& S = segs[k];
     DRPO_REQUIRE(S.p && S.end >= S.start && (!S.adam || (S.g && S.m && S.v)), "drpo_optim_step: bad segment %d", k);
     DRPO_REQUIRE(!S.grad_from_sum || S.grad_sum_rows >= 1, "drpo_optim_step: segment %d: grad_sum_rows", k);
     a.seg[k] = S;
-    a.first[k] = tot;
-    tot += (S.end - S.start + OPT_BLOCK_ELEMS - 1) / OPT_BLOCK_ELEMS;
+    if (S.end == S.start) continue;
+    const int rc = plan_segment(S, k, a, tot);
+    if (rc != DRPO_OK) return rc;
   }
-  a.first[n] = tot;
-  a.n = n;
   if (tot == 0) return DRPO_OK;
   optim_step_kernel<<<(unsigned)tot, 256, 0, stream>>>(a);
   DRPO_LAUNCH_CHECK("optim_step");

@@ -36,7 +36,7 @@ namespace {
 constexpr int WG_NW = 4;                 // waves per workgroup
 constexpr int WG_NT = WG_NW * 64;
 #ifndef DRPO_WG_D
-#define DRPO_WG_D 5
+#define DRPO_WG_D 3
 #endif
 constexpr int WG_D = DRPO_WG_D;          // register ring slots (k-groups of 4 rows each; A/B macro)
 constexpr int WG_ROWQ = 64;              // chunk granularity (rows)
@@ -82,6 +82,7 @@ struct WgradPlan {
 constexpr int WG_MAXSUMS = 4;
 
 struct WgradArgs {
+  int64_t first[WG_MAXITEMS];        // first logical workgroup per item (unused: INT64_MAX)
   drpo_wgrad_item_t it[WG_MAXITEMS];
   WgradPlan pl[WG_MAXITEMS];
   int64_t units;
@@ -313,6 +314,20 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
   float* gW = I.gW + (size_t)zb * I.gwstride;
   float* gb = I.gb + (size_t)zb * I.gbstride;
   float* red = lds + WG_NW * NA * WG_SLD + WG_NW * TO;   // 4 floats
+  // the gradient's current values: loaded by the workgroup that finishes the tile,
+  // before (and in flight with) the slab loads; every load precedes the first store
+  float gv[E];
+  const bool bias_mine = do_bias && tid < TO && o0 + tid < dout;
+  float gbv = 0.f;
+  auto load_grad = [&]() {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int idx = tid + WG_NT * e;
+      const int o = o0 + idx / TI, i = i0 + idx % TI;
+      gv[e] = (o < dout && i < din) ? gW[(size_t)o * din + i] : 0.f;
+    }
+    gbv = bias_mine ? gb[o0 + tid] : 0.f;
+  };
   if (P.nch > 1) {
     float* my = a.slab + P.slab_off + (tile_local * P.nch + ch) * SL;
 #pragma unroll
@@ -331,28 +346,37 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
     __syncthreads();
     STAMPG(3);
     if (!s_last) return;
-    // last arriver: the tile's partials in chunk order
+    load_grad();
+    // last arriver: the tile's partials in chunk order, CG chunks' loads in flight at a
+    // time (one memory round trip per group of chunks, not per chunk)
     const float* base = a.slab + P.slab_off + tile_local * P.nch * SL;
+    const bool bias_lane = do_bias && tid < TO;
 #pragma unroll
     for (int e = 0; e < E; ++e) pv[e] = 0.f;
     pb = 0.f;
-    for (int c = 0; c < P.nch; ++c) {
+    constexpr int CG = E >= 16 ? 4 : 8;
+    for (int c0 = 0; c0 < P.nch; c0 += CG) {
+      float t[CG][E], tb[CG];
 #pragma unroll
-      for (int e = 0; e < E; ++e) pv[e] += ld_sc1(base + c * SL + tid + WG_NT * e);
-      if (do_bias && tid < TO) pb += ld_sc1(base + c * SL + TO * TI + tid);
+      for (int u = 0; u < CG; ++u) {
+        const int c = min(c0 + u, P.nch - 1);     // clamped: a duplicate load, not added
+#pragma unroll
+        for (int e = 0; e < E; ++e) t[u][e] = ld_sc1(base + c * SL + tid + WG_NT * e);
+        tb[u] = bias_lane ? ld_sc1(base + c * SL + TO * TI + tid) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CG; ++u) {
+        if (c0 + u < P.nch) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) pv[e] += t[u][e];
+          pb += tb[u];
+        }
+      }
     }
+  } else {
+    load_grad();
   }
-  // gradient += sum (the caller's gradient is zeroed or holds terms to accumulate);
-  // every load is issued before the first store
-  float gv[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int idx = tid + WG_NT * e;
-    const int o = o0 + idx / TI, i = i0 + idx % TI;
-    gv[e] = (o < dout && i < din) ? gW[(size_t)o * din + i] : 0.f;
-  }
-  const bool bias_mine = do_bias && tid < TO && o0 + tid < dout;
-  const float gbv = bias_mine ? gb[o0 + tid] : 0.f;
+  // gradient += sum (the caller's gradient is zeroed or holds terms to accumulate)
   float sq = 0.f;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -397,8 +421,11 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs a) {
     else if (a.nsums) sums_block(a, wsm);
     return;
   }
+  // the item: the number of item starts <= bid, all read at once (independent scalar
+  // loads, one kernarg round trip; a dependent search costs one per item passed)
   int q = 0;
-  while (q + 1 < a.n && bid >= a.pl[q + 1].first_unit) ++q;
+#pragma unroll
+  for (int i = 1; i < WG_MAXITEMS; ++i) q += bid >= a.first[i] ? 1 : 0;
   const WgradPlan& P = a.pl[q];
   const int64_t u = bid - P.first_unit;
   if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
@@ -505,6 +532,7 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     tile += ntile;
     if (P.nch > 1) slab += ntile * P.nch * ((int64_t)s.to * s.ti + s.to);
   }
+  for (int k = 0; k < WG_MAXITEMS; ++k) a.first[k] = k < m ? a.pl[k].first_unit : INT64_MAX;
   a.units = unit;
   p.tiles = tile;
   p.slab = slab;

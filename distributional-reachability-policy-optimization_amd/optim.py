@@ -7,6 +7,7 @@ arithmetic runs in one HIP kernel per clip segment (csrc/optim.hip).
 ``CosineAnnealingLR`` reproduces torch's recursive (chainable) schedule, which is
 host-side scalar logic in the reference too.
 """
+import ctypes
 import math
 
 import torch
@@ -93,6 +94,8 @@ class Adam:
         if ema is not None:
             sg.ema_target, sg.ema_rate, sg.ema_keep = ema[0].data_ptr(), float(ema[1]), float(1.0 - float(ema[1]))
         sg.map = 0 if pack_map is None else pack_map.data_ptr()
+        host = getattr(pack_map, 'host', None)
+        sg.map_host = 0 if host is None else ctypes.addressof(host)
         if grad_from_sum is not None:
             sg.grad_from_sum, sg.grad_sum_rows = grad_from_sum[0].data_ptr(), int(grad_from_sum[1])
             sg.grad_from_sum_kind = int(grad_from_sum_kind)
@@ -165,6 +168,8 @@ def ema_segment(p, start, end, target, rate, pack_map=None):
     sg.p, sg.start, sg.end, sg.adam = p.data_ptr(), start, end, 0
     sg.ema_target, sg.ema_rate, sg.ema_keep = target.data_ptr(), float(rate), float(1.0 - float(rate))
     sg.map = 0 if pack_map is None else pack_map.data_ptr()
+    host = getattr(pack_map, 'host', None)
+    sg.map_host = 0 if host is None else ctypes.addressof(host)
     sg.grad_scale = 1.0
     return sg
 

@@ -100,6 +100,7 @@ class FlatGroup:
         mp.Pt = target.packed.data_ptr() if target is not None else 0
         raw = bytes(mp)
         dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.data.device)
+        dev.host = mp          # the host copy plans the optimizer's 4x4-block work split
         cache[key] = dev
         return dev
 

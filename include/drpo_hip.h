@@ -518,6 +518,11 @@ typedef struct {
                                  parallel mean into the step after a SUM all-reduce. 0 is
                                  read as 1, so zero-initialised descriptors keep plain grads */
   int grad_sum_n;             /* grad_from_sum holds this many partial sums, added in order (0 = 1) */
+  const drpo_pack_map_t* map_host; /* optional host copy of *map: the launch then covers each
+                                 weight matrix in 4x4 blocks (16-byte loads / stores per row,
+                                 16-byte mirror stores per row and per column) instead of
+                                 runs of 4 flat elements with scattered transposed-mirror
+                                 stores */
 } drpo_optim_seg_t;
 
 int drpo_optim_step(const drpo_optim_seg_t* segs /* host, <= 8 */, int n, drpo_stream_t stream);
