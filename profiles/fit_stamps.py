@@ -30,31 +30,36 @@ def main():
     m.fit(alg.replay_buffer, steps=1)
     torch.cuda.synchronize()
     L.drpo_debug_stamps(buf.ctypes.data, n)
-    st = buf[32768:32768 + 4096, 0:5].astype(np.int64)   # STAMPW rows (csrc/mlp.hip)
-    nwg = int((st[:, 4] > 0).sum())
-    st = st[:nwg]
-    t0 = st[:, 0].min()
-    print(f'== mlp_wgrad_kernel (fit step, config 2): {nwg} workgroups')
-    print(f'   start offsets (cycles) pct 0/25/50/75/100: {np.percentile(st[:, 0] - t0, [0, 25, 50, 75, 100]).astype(int)}')
-    print(f'   end offsets   (cycles) pct 0/25/50/75/100: {np.percentile(st[:, 4] - t0, [0, 25, 50, 75, 100]).astype(int)}')
-    names = ['first stage loaded', 'stage loop', 'wave reduce', 'atomics + bias']
-    for c in range(1, 5):
-        d = st[:, c] - st[:, c - 1]
-        print(f'   {names[c - 1]:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
-    d = st[:, 4] - st[:, 0]
+    # forward (mlp_fwd_kernel STAMP rows 0..: 0 start, 1 input staged, 2/3 trunk layers,
+    # 6/7 head 1 layers (lb.y == 0), 10/11 head 2 layers (lb.y == 1))
+    fw = buf[0:4096].astype(np.int64)
+    nf = int((fw[:, 0] > 0).sum())
+    fw = fw[:nf]
+    print(f'== mlp_fwd_kernel (fit step, split heads): {nf} workgroups')
+    for a, b, name in ((0, 1, 'stage input'), (1, 2, 'trunk L1'), (2, 3, 'trunk L2'), (3, 6, 'head1 L1'),
+                       (6, 7, 'head1 L2'), (3, 10, 'head2 L1'), (10, 11, 'head2 L2')):
+        ok = (fw[:, a] > 0) & (fw[:, b] > 0)
+        if ok.any():
+            d = fw[ok, b] - fw[ok, a]
+            print(f'   {name:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc  (n={ok.sum()})')
+    end = np.maximum(fw[:, 7], fw[:, 11])
+    d = end - fw[:, 0]
     print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
-    bw = buf[32768:32768 + 4096, 5:14].astype(np.int64)
-    nb = int((bw[:, 8] > 0).sum())
+    bw = buf[32768:32768 + 4096].astype(np.int64)
+    nb = int((bw[:, 0] > 0).sum())
     bw = bw[:nb]
-    print(f'== mlp_bwd_kernel (fit step, trunk + 2 heads): {nb} workgroups')
-    names = ['head 1 gout load', 'head 1 backward', 'head 1 add to dT', 'head 2 gout load', 'head 2 backward',
-             'head 2 add to dT', 'trunk backward', 'dx store']
-    for c in range(1, 9):
-        d = bw[:, c] - bw[:, c - 1]
-        print(f'   {names[c - 1]:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
-    d = bw[:, 8] - bw[:, 0]
-    print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
-
+    print(f'== mlp_bwd_ens_kernel (fit step, paired heads + NLL upstream): {nb} workgroups')
+    for a, b, name in ((0, 5, ' start -> NLL loop'), (5, 6, ' NLL element loop'), (6, 7, ' mse wave sums'),
+                       (7, 1, ' partials + barrier'), (0, 1, 'NLL upstream'), (1, 2, 'heads out bwd'), (2, 3, 'hidden act grad'),
+                       (3, 4, 'heads -> trunk catK'), (4, 12, 'trunk backward')):
+        ok = (bw[:, a] > 0) & (bw[:, b] > 0)
+        if ok.any():
+            d = bw[ok, b] - bw[ok, a]
+            print(f'   {name:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc  (n={ok.sum()})')
+    ok = bw[:, 12] > 0
+    if ok.any():
+        d = bw[ok, 12] - bw[ok, 0]
+        print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
 
 if __name__ == '__main__':
     main()
