@@ -115,33 +115,6 @@ __device__ __forceinline__ float* run_net(const drpo_mlp_fwd_t& a, float* in, fl
   return cur;
 }
 
-#ifndef DRPO_TOUCH
-#define DRPO_TOUCH 1   // A/B macro: 0 builds the kernels without the warm-up touches
-#endif
-
-// Warm-up touch of a layer's first two k-steps of this wave's first column block and
-// of its bias (4-byte loads spread over the 1 KB fragments: every cache line of them):
-// issued before the input staging, so each layer's first weight fragments are L2 hits
-// when its k-loop starts instead of HBM + page-walk round trips paid layer by layer
-// (fit forward stamps: the 1-k-step first layer alone cost 7 k cycles).
-__device__ __forceinline__ float touch_layer(const drpo_mlp_layer_t& L, int z) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int NCB = (L.dout + 15) >> 4, NKS = (L.din + 15) >> 4;
-  const int cb = wave < NCB ? wave : NCB - 1;
-  const float* P = L.W + (size_t)z * L.wstride + ((size_t)cb * NKS << 8) + (lane << 2);
-  float t = gload(P);
-  if (NKS > 1) t += gload(P + 256);
-  return t + gload(L.b + (size_t)z * L.bstride + (lane < L.dout ? lane : 0));
-}
-template <int NI>
-__device__ __forceinline__ float touch_net(const drpo_mlp_fwd_t& a, int z) {
-  float t = 0.f;
-#pragma unroll
-  for (int l = 0; l < MAXL; ++l)
-    if (l < a.net[NI].nl) t += touch_layer(a.net[NI].L[l], z);
-  return t;
-}
-
 __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xin = smem;                       // ROWS x LDH
@@ -162,13 +135,6 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
   const bool split = a.trunk && a.split_heads;
   const bool tsave = !split || lb.y == 0;
   STAMP(0);
-  // this workgroup's layers (trunk mode: the trunk, then its head(s))
-  float warm = 0.f;
-  if (!DRPO_TOUCH) {
-  } else if (!a.trunk) warm = lb.y == 0 ? touch_net<0>(a, z) : (lb.y == 1 ? touch_net<1>(a, z) : touch_net<2>(a, z));
-  else if (split) warm = touch_net<0>(a, z) + (lb.y == 0 ? touch_net<1>(a, z) : touch_net<2>(a, z));
-  else warm = touch_net<0>(a, z) + (a.nnets > 1 ? touch_net<1>(a, z) : 0.f) + (a.nnets > 2 ? touch_net<2>(a, z) : 0.f);
-
   for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
     const int r = e / kpad, k = e - r * kpad;
     float v = 0.f;
@@ -191,7 +157,6 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
     }
     xin[r * LDH + k] = v;
   }
-  asm volatile("" ::"v"(warm));   // the touches complete with the staging loads
   lds_barrier();
   STAMP(1);
   if (!a.trunk) {
@@ -796,17 +761,6 @@ __device__ __forceinline__ void squash_upstream(ActorHeadK& h, int side, const d
   if (side == 0 && h.alpha_sum) wg_loss_partial(asum, h.alpha_sum + row0 / FW_ROWS);
 }
 
-// warm-up touch of a backward-data layer's transposed mirror (first two k-steps of this
-// wave's first column block; see touch_layer)
-__device__ __forceinline__ float touch_bwd_layer(const drpo_mlp_bwd_layer_t& L, int z) {
-  // wave-uniform fragment base (scalar registers) + the lane offset: one VGPR per touch
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int NCB = (L.din + 15) >> 4, NKS = (L.dout + 15) >> 4;
-  const int cb = wave < NCB ? wave : NCB - 1;
-  const float* P = L.W + (size_t)z * L.wstride + ((size_t)cb * NKS << 8);
-  return gload(P + ((threadIdx.x & 63) << 2));
-}
-
 // upstream families compiled into a backward kernel instantiation (each launch kind
 // gets only the producer code it uses, so none of them adds register pressure -- and
 // spills -- to the others' GEMM phases)
@@ -822,12 +776,6 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
   const int hid = h1.L[0].dout, out = h1.L[1].dout;
   const int opad = round_up(out, 16), hpad = round_up(hid, 16);
   float sv1[BW_PER], sv2[BW_PER];
-  // every later product's first weight fragments, in flight with the upstream's loads
-  const drpo_mlp_bwd_net_t& tr = a.net[0];
-  float warm = 0.f;
-  if (DRPO_TOUCH)
-    warm = touch_bwd_layer(h1.L[1], z) + touch_bwd_layer(h2.L[1], z) + touch_bwd_layer(h1.L[0], z) +
-           touch_bwd_layer(h2.L[0], z) + touch_bwd_layer(tr.L[tr.nl - 1], z);
   bwd_fetch_act(h1.L[0], z, a.rows, row0, nrows, sv1);   // head 1's hidden saved values, one phase ahead
   // output layers (identity): dZ = the given output gradient, saved for the weight gradients
   const size_t so = ((size_t)z * a.rows + row0) * out;
@@ -853,7 +801,6 @@ __device__ __forceinline__ void bwd_heads_paired(const drpo_mlp_bwd_t& __restric
     }
     (w ? bA : G)[r * LDH + k] = gv;
   }
-  asm volatile("" ::"v"(warm));
   lds_barrier();
   STAMPW(1);
   // dY(hidden) of both heads: one two-input pair layer (K = out)
