@@ -158,7 +158,7 @@ class WgradItem(ctypes.Structure):
     """drpo_wgrad_item_t"""
     _fields_ = [('dz', P), ('y', P), ('gW', P), ('gb', P), ('dout', c_int), ('din', c_int), ('rows', c_int64),
                 ('zstride', c_int64), ('ystride', c_int64), ('gwstride', c_int64), ('gbstride', c_int64),
-                ('nbatch', c_int), ('sq', P), ('sq_off', c_int)]
+                ('nbatch', c_int), ('sq', P), ('sq_off', c_int), ('dz2', P)]
 
 
 class BufferView(ctypes.Structure):

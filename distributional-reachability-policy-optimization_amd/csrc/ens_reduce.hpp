@@ -11,7 +11,9 @@ constexpr int LOSS_MAXS1 = 256;
 // spread over 16 lanes (strided partials, then a fixed xor tree), so the kernel waits
 // a couple of memory latencies instead of one per partial; the order is fixed, so the
 // result is deterministic.
-__device__ __forceinline__ void ens_loss_reduce_block(const drpo_ens_reduce_t& rd) {
+// Reduce: drpo_ens_reduce_t, in generic memory or read in place from a kernarg segment
+template <typename Reduce>
+__device__ __forceinline__ void ens_loss_reduce_block(Reduce& rd) {
   const float* __restrict__ part = rd.part;
   const int nbx = rd.nbx, Z = rd.Z, S1 = rd.S1;
   const float* __restrict__ minlv = rd.minlv;

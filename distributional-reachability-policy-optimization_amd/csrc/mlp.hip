@@ -598,9 +598,12 @@ typedef const __attribute__((address_space(4))) drpo_ens_upstream_t EnsUpK;
 // gradients) at partial block (z, bx) of the drpo_ens_loss workspace layout. Cm / Cx:
 // LDS scratch (16 rows each). Thread t owns column t % 16-padded-width of row t / width,
 // the element mapping and summation order of ens_loss_kernel at S+1 <= 16.
+// split < 0: both heads (paired backward; the output layers' dZ saved here). split = h
+// (split-heads backward, one workgroup per head): the output layers' dZ are saved by the
+// head's own backward pass, and only head 0's workgroup writes the loss partials.
 __device__ __forceinline__ void ens_upstream(EnsUpK& u, const drpo_mlp_bwd_net_t& hd, const drpo_mlp_bwd_net_t& hl,
                                              float* Gd, float* Gl, float* Cm, float* Cx, int z, int bx, int row0,
-                                             int nrows) {
+                                             int nrows, int split = -1) {
   const int tid = threadIdx.x;
   const int S = u.S, S1 = S + 1, opad = round_up(S1, 16);
   const int64_t b = u.b;
@@ -628,8 +631,8 @@ __device__ __forceinline__ void ens_upstream(EnsUpK& u, const drpo_mlp_bwd_net_t
       gl = dl * s1 * s2;
       cmn = dl * (1.f - s1);
       cmx = dl * s1 * (1.f - s2);
-      if (hd.L[1].dz) gstore(hd.L[1].dz + o, gd);
-      if (hl.L[1].dz) gstore(hl.L[1].dz + o, gl);
+      if (split < 0 && hd.L[1].dz) gstore(hd.L[1].dz + o, gd);
+      if (split < 0 && hl.L[1].dz) gstore(hl.L[1].dz + o, gl);
     }
     Gd[r * LDH + k] = gd;
     Gl[r * LDH + k] = gl;
@@ -649,6 +652,7 @@ __device__ __forceinline__ void ens_upstream(EnsUpK& u, const drpo_mlp_bwd_net_t
   float* part_min = part_mse + (size_t)u.Z * nbx;
   float* part_max = part_min + (size_t)u.Z * nbx * S1;
   const size_t pb = (size_t)z * nbx + bx;
+  if (split > 0) return;
   if (tid == 0) {
     float t = 0.f;
     for (int w = 0; w < FW_NW; ++w) t += s_red[w];
@@ -929,9 +933,23 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     // head sel + 1 alone: the trunk gradient is linear in the head gradients, so its
     // share backs through the trunk here (dz for head 1, dz2 for head 2)
     const drpo_mlp_bwd_net_t& n = a.net[sel + 1];
-    load_gout(n, G);
+    bool up = false;
+    if constexpr ((UPF & UPF_ENS) != 0) {
+      if (eu && a.upstream == DRPO_UPSTREAM_ENS) {
+        // both heads' NLL gradients are formed (they share the element's terms); this
+        // workgroup keeps its own head's in G
+        ens_upstream(*eu, a.net[1], a.net[2], sel == 0 ? G : bA, sel == 0 ? bA : G, bB, DT, z, row0 / FW_ROWS, row0,
+                     nrows, sel);
+        lds_barrier();   // Cm / Cx (bB, DT) are read by the partial sums above; bwd_net reuses bB
+        up = true;
+      }
+    }
+    if (!up) load_gout(n, G);
+    STAMPW(1);
     float* gh = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, true);
+    STAMPW(2);
     bwd_net(a.net[0], gh, bA, bB, z, a.rows, row0, nrows, false, sel == 1);
+    STAMPW(12);
     return;
   }
   if (bwd_paired_heads(a)) {
@@ -1052,9 +1070,15 @@ DRPO_API int drpo_mlp_backward_ens(const drpo_mlp_bwd_t* a, const drpo_ens_upstr
                                    drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(a && up && red_in && reduce_out, "drpo_mlp_backward_ens: null argument");
-  DRPO_REQUIRE(a->upstream == DRPO_UPSTREAM_ENS && a->trunk && a->nnets == 3 && !a->split_heads &&
-                   a->nbatch == up->Z && a->rows == up->b,
-               "drpo_mlp_backward_ens: the descriptor must be the ensemble trunk + paired heads with upstream ENS");
+  DRPO_REQUIRE(a->upstream == DRPO_UPSTREAM_ENS && a->trunk && a->nnets == 3 && a->nbatch == up->Z &&
+                   a->rows == up->b,
+               "drpo_mlp_backward_ens: the descriptor must be the ensemble trunk + two heads with upstream ENS");
+  if (a->split_heads) {   // one workgroup per (row tile, head): the trunk dZ leaves as dz + dz2
+    DRPO_REQUIRE(!a->net[0].dx, "drpo_mlp_backward_ens: split heads and a trunk input gradient");
+    for (int l = 0; l < a->net[0].nl; ++l)
+      DRPO_REQUIRE(!a->net[0].L[l].dz == !a->net[0].L[l].dz2,
+                   "drpo_mlp_backward_ens: split heads: trunk layer %d needs dz2 with dz", l);
+  }
   const drpo_mlp_bwd_net_t &h1 = a->net[1], &h2 = a->net[2];
   DRPO_REQUIRE(h1.nl == 2 && h2.nl == 2 && h1.L[1].dout == up->S + 1 && h2.L[1].dout == up->S + 1 &&
                    up->S + 1 <= 64 && h1.L[1].act == ACT_NONE && h2.L[1].act == ACT_NONE &&
@@ -1077,7 +1101,7 @@ DRPO_API int drpo_mlp_backward_ens(const drpo_mlp_bwd_t* a, const drpo_ens_upstr
   reduce_out->maxlv = up->maxlv;
   reduce_out->gscale = up->gscale;
   BwdEnsArgs m{*a, *up};
-  dim3 grid((unsigned)nbx, 1, a->nbatch);
+  dim3 grid((unsigned)nbx, a->split_heads ? 2 : 1, a->nbatch);
   mlp_bwd_ens_kernel<<<grid, FW_NT, bwd_lds(), stream>>>(m);
   DRPO_LAUNCH_CHECK("mlp_backward_ens");
   return DRPO_OK;

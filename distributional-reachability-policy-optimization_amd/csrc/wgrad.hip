@@ -74,6 +74,7 @@ struct WgradPlan {
   int nto, nti, nch;       // tiles along outputs / inputs, row chunks
   int chunk;               // rows per chunk (multiple of WG_ROWQ)
   int va, vb;              // 16-byte loads of dZ / Y rows (widths % 4 == 0, aligned)
+  int z2;                  // a second dZ term (item dz2)
   int64_t first_unit;      // first logical workgroup of the item
   int64_t first_tile;      // first arrival counter of the item
   int64_t slab_off;        // first slab float of the item (tiles with nch > 1)
@@ -95,11 +96,16 @@ struct WgradArgs {
   unsigned* ctr;
 };
 
+// The launch arguments are read in place from the kernarg segment (address space 4,
+// scalar loads): with the by-value parameter the compiler copies the 3 KB struct to
+// scratch once the kernel's code grows (dynamic item index + many instantiations).
+typedef const __attribute__((address_space(4))) WgradArgs WgradArgsK;
+
 // *out = part[0] + ... + part[n-1] for every entry, in a fixed order (256 strided
 // lanes, then a fixed tree): deterministic, no float atomics
-__device__ __forceinline__ void sums_block(const WgradArgs& a, float* red) {
+__device__ __forceinline__ void sums_block(WgradArgsK& a, float* red) {
   for (int q = 0; q < a.nsums; ++q) {
-    const drpo_sum_t& S = a.sums[q];
+    const auto& S = a.sums[q];
     float v = 0.f;
     for (int j = threadIdx.x; j < S.n; j += WG_NT) v += S.part[j];
     red[threadIdx.x] = v;
@@ -192,13 +198,13 @@ __device__ __forceinline__ float wg_block_sum(float v, float* red) {
   return s;   // valid in thread 0
 }
 
-template <int TO, int TI, bool VA, bool VB>
-__device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u, float* lds) {
+template <int TO, int TI, bool VA, bool VB, bool Z2>
+__device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, float* lds) {
   constexpr int MA = TO / 16, MB = TI / 16, NA = MA * MB;
   constexpr int WA = TO == 64 ? 4 : 1, WB = TI == 64 ? 4 : 1;
   constexpr int E = TO * TI / WG_NT;          // tile elements per thread (16, 4 or 1)
-  const drpo_wgrad_item_t& I = a.it[q];
-  const WgradPlan& P = a.pl[q];
+  const auto& I = a.it[q];
+  const auto& P = a.pl[q];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, l15 = lane & 15;
   const int it_i = (int)(u % P.nti);
@@ -210,6 +216,7 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
   const int64_t tile_local = ((int64_t)zb * P.nto + it_o) * P.nti + it_i;
   const int dout = I.dout, din = I.din;
   const float* __restrict__ dz = I.dz + (size_t)zb * I.zstride;
+  const float* __restrict__ dz2 = Z2 ? I.dz2 + (size_t)zb * I.zstride : nullptr;
   const float* __restrict__ y = I.y + (size_t)zb * I.ystride;
   const int o0 = it_o * TO, i0 = it_i * TI;
   const int64_t r0 = (int64_t)ch * P.chunk;
@@ -231,13 +238,15 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
   // wave k-group j covers rows r0 + 16 j + 4 wave + (0..3); lane group g takes row 4.. + g
   const int nj = P.chunk / (4 * WG_NW);      // k-groups per wave
   const int64_t rlane = r0 + 4 * wave + g;
-  auto ld = [&](int j, f32x4& fa, f32x4& fb) {
+  auto ld = [&](int j, f32x4& fa, f32x4& fb, f32x4& fa2) {
     const int64_t r = rlane + 16 * (int64_t)j;
     const int64_t rc = r < r1 ? r : r1 - 1;
     fa = frag_load<WA, VA>(dz, rc, dout, ca, dout);
     fb = frag_load<WB, VB>(y, rc, din, cb, din);
+    if constexpr (Z2) fa2 = frag_load<WA, VA>(dz2, rc, dout, ca, dout);
   };
-  auto use = [&](int j, f32x4 fa, const f32x4& fb) {
+  auto use = [&](int j, f32x4 fa, const f32x4& fb, const f32x4& fa2) {
+    if constexpr (Z2) fa += fa2;   // the two dZ terms, added at use (see frag_load)
     if (rlane + 16 * (int64_t)j >= r1) fa = f32x4{0.f, 0.f, 0.f, 0.f};   // row past the chunk
     frag_mma<TO, TI>(fa, fb, acc);
     if (do_bias) bsum += fa;
@@ -246,18 +255,21 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
   // k-group s - (D - 1) (D - 1 k-groups of cover). Every load is inside the loop: with
   // a prologue of loads outside it the compiler drains vmcnt at every loop entry. Steps
   // past the chunk load clamped rows that are never consumed or are zeroed at use.
-  f32x4 ra[WG_D], rb[WG_D];
+  f32x4 ra[WG_D], rb[WG_D], ra2[Z2 ? WG_D : 1];
 #pragma unroll
   for (int v = 0; v < WG_D; ++v) ra[v] = rb[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int v = 0; v < (Z2 ? WG_D : 1); ++v) ra2[v] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int steps = (nj + WG_D - 1 + WG_D - 1) / WG_D * WG_D;
   for (int s0 = 0; s0 < steps; s0 += WG_D) {
 #pragma unroll
     for (int v = 0; v < WG_D; ++v) {
-      ld(s0 + v, ra[v], rb[v]);
+      ld(s0 + v, ra[v], rb[v], ra2[Z2 ? v : 0]);
       // keep the prefetch here: the scheduler would otherwise sink the loads past the
       // MFMAs, next to their first use
       __builtin_amdgcn_sched_barrier(0);
-      if (s0 + v >= WG_D - 1) use(s0 + v - (WG_D - 1), ra[(v + 1) % WG_D], rb[(v + 1) % WG_D]);
+      if (s0 + v >= WG_D - 1)
+        use(s0 + v - (WG_D - 1), ra[(v + 1) % WG_D], rb[(v + 1) % WG_D], ra2[Z2 ? (v + 1) % WG_D : 0]);
     }
 #ifdef DRPO_STAMPS
     if (s0 == WG_D) STAMPG(5);   // the first k-group consumed: the ring's fill latency
@@ -400,17 +412,25 @@ __device__ __forceinline__ void wgrad_unit(const WgradArgs& a, int q, int64_t u,
   STAMPG(4);
 }
 
-template <int TO, int TI>
-__device__ __forceinline__ void wgrad_unit_v(const WgradArgs& a, int q, int64_t u, float* lds) {
-  const WgradPlan& P = a.pl[q];
-  if (P.va && P.vb) wgrad_unit<TO, TI, true, true>(a, q, u, lds);
-  else if (P.va) wgrad_unit<TO, TI, true, false>(a, q, u, lds);
-  else if (P.vb) wgrad_unit<TO, TI, false, true>(a, q, u, lds);
-  else wgrad_unit<TO, TI, false, false>(a, q, u, lds);
+template <int TO, int TI, bool Z2>
+__device__ __forceinline__ void wgrad_unit_z(WgradArgsK& a, int q, int64_t u, float* lds) {
+  const auto& P = a.pl[q];
+  if (P.va && P.vb) wgrad_unit<TO, TI, true, true, Z2>(a, q, u, lds);
+  else if (P.va) wgrad_unit<TO, TI, true, false, Z2>(a, q, u, lds);
+  else if (P.vb) wgrad_unit<TO, TI, false, true, Z2>(a, q, u, lds);
+  else wgrad_unit<TO, TI, false, false, Z2>(a, q, u, lds);
 }
 
-__global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs a) {
+template <int TO, int TI>
+__device__ __forceinline__ void wgrad_unit_v(WgradArgsK& a, int q, int64_t u, float* lds) {
+  if (a.pl[q].z2) wgrad_unit_z<TO, TI, true>(a, q, u, lds);
+  else wgrad_unit_z<TO, TI, false>(a, q, u, lds);
+}
+
+__global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs args) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
+  WgradArgsK& a = *(const __attribute__((address_space(4))) WgradArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)args;
   // logical order: item, then (member, chunk, o-tile, i-tile) with i fastest, spread so
   // that each XCD runs one contiguous range: the units of one row chunk (which read the
   // same dZ / Y rows) share an L2
@@ -426,7 +446,7 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs a) {
   int q = 0;
 #pragma unroll
   for (int i = 1; i < WG_MAXITEMS; ++i) q += bid >= a.first[i] ? 1 : 0;
-  const WgradPlan& P = a.pl[q];
+  const auto& P = a.pl[q];
   const int64_t u = bid - P.first_unit;
   if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
   else if (P.to == 64) wgrad_unit_v<64, 16>(a, q, u, wsm);
@@ -522,7 +542,8 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     WgradPlan& P = a.pl[k];
     const drpo_wgrad_item_t& I = a.it[k];
     P.to = s.to; P.ti = s.ti; P.nto = s.nto; P.nti = s.nti; P.nch = nch[k]; P.chunk = chunk[k];
-    P.va = (I.dout & 3) == 0 && ((uintptr_t)I.dz & 15) == 0 && (I.zstride & 3) == 0;
+    P.va = (I.dout & 3) == 0 && ((uintptr_t)I.dz & 15) == 0 && ((uintptr_t)I.dz2 & 15) == 0 && (I.zstride & 3) == 0;
+    P.z2 = I.dz2 != nullptr;
     P.vb = (I.din & 3) == 0 && ((uintptr_t)I.y & 15) == 0 && (I.ystride & 3) == 0;
     P.first_unit = unit;
     P.first_tile = tile;

@@ -34,11 +34,11 @@ from ._abi import EnsReduce, EnsUpstream, WgradItem
 # members) would leave most of the 256 CUs idle. The trunk is recomputed per head
 # (1.33x the forward FLOPs) but each workgroup's serial chain shortens from 5 to 3
 # dense layers: fit forward 28.8 -> 20.1 us at E=7, b=256 (csrc/mlp.hip, split_heads).
-# Backward: the same split (2 instead of 4 dense layers per workgroup, 33.8 -> 22.7 us)
-# leaves the trunk dZ as two terms, and the weight-gradient pass then re-reads the
-# trunk activations once per term (21 -> 38 us); measured and rejected in round 2. The
-# fit's backward now also forms the NLL gradients in-kernel from both heads' outputs
-# (drpo_mlp_backward_ens, paired heads), so the split backward is not offered.
+# Backward: the same split -- one workgroup per (row tile, head), each forming the NLL
+# gradient of its head in-kernel (drpo_mlp_backward_ens) and backing its share through
+# the trunk -- leaves the trunk dZ as two terms (dz + dz2). The weight-gradient launch
+# takes both terms as ONE item (drpo_wgrad_item_t.dz2: the product (dz + dz2)^T y reads
+# the trunk activations once; round 2's two-item form re-read them and was rejected).
 SPLIT_HEADS_MAX_TILES = 256
 
 
@@ -49,7 +49,9 @@ def split_heads(n, Z):
 
 
 def split_heads_bwd(n, Z):
-    return False
+    if os.environ.get('DRPO_SPLIT_BWD', '1') == '0':     # A/B knob: the paired backward
+        return False
+    return split_heads(n, Z)
 
 
 class EnsembleEngine:
@@ -248,27 +250,23 @@ class EnsembleEngine:
 
     def _backward_descs(self, nets, strides, save_x, gD, gL, b, Z):
         """Backward-data descriptor and the weight-gradient items: (desc, [(items, n)]).
-        Split heads (DRPO_SPLIT_BWD, an A/B knob) leave the trunk dZ as two terms; the
-        second term's items go in a second launch (one launch never has two items on
-        one gradient)."""
+        Split heads (split_heads_bwd) leave the trunk dZ as two terms, which the trunk
+        layers' items carry as dz + dz2."""
         split = nets[0].dz2[0] is not None
         d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides, split_heads=split)
-        items, extra = [], []
+        items = []
         trunk_out = nets[0].sy[-1]
         for j, net in enumerate(nets):
             ins = [save_x if j == 0 else trunk_out] + [net.sy[l] for l in range(len(net.layers) - 1)]
             for l, (W, bb, din, dout, act, _) in enumerate(net.layers):
                 gW, gb = net.grad_layers[l]
-                for dz, dst in ((net.dz[l], items), (net.dz2[l], extra)):
-                    if dz is None:
-                        continue
-                    it = WgradItem()
-                    it.dz, it.y, it.gW, it.gb = dz.data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
-                    it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
-                    it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
-                    dst.append(it)
-        launches = [((WgradItem * len(x))(*x), len(x)) for x in (items, extra) if x]
-        return d, launches
+                it = WgradItem()
+                it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
+                it.dz2 = 0 if net.dz2[l] is None else net.dz2[l].data_ptr()
+                it.dout, it.din, it.rows, it.nbatch = dout, din, b, Z
+                it.zstride, it.ystride, it.gwstride, it.gbstride = b * dout, b * din, dout * din, dout
+                items.append(it)
+        return d, [((WgradItem * len(items))(*items), len(items))]
 
     def _wgrad_ws(self, key, arr, n):
         """Per-call-site weight-gradient workspace (sized once per descriptor array)."""

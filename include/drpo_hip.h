@@ -261,6 +261,9 @@ typedef struct {
                       FINISHED gradient (weights + bias) of output tile t of this item,
                       t < drpo_mlp_wgrad_tiles(item) (summed by drpo_optim_step) */
   int sq_off;
+  const float* dz2;  /* optional second dL/dZ term, same layout as dz: the product is
+                        (dz + dz2)^T y (a split-heads backward leaves the trunk's dZ as
+                        the sum of the two heads' shares) */
 } drpo_wgrad_item_t;
 
 /* the reduction step of drpo_ens_loss, as data: run by drpo_mlp_wgrad_reduce */

@@ -48,10 +48,13 @@ def main():
     bw = buf[32768:32768 + 4096].astype(np.int64)
     nb = int((bw[:, 0] > 0).sum())
     bw = bw[:nb]
-    print(f'== mlp_bwd_ens_kernel (fit step, paired heads + NLL upstream): {nb} workgroups')
-    for a, b, name in ((0, 5, ' start -> NLL loop'), (5, 6, ' NLL element loop'), (6, 7, ' mse wave sums'),
-                       (7, 1, ' partials + barrier'), (0, 1, 'NLL upstream'), (1, 2, 'heads out bwd'), (2, 3, 'hidden act grad'),
-                       (3, 4, 'heads -> trunk catK'), (4, 12, 'trunk backward')):
+    split = nb > 0 and bw[:, 3].max() == 0     # split heads: stamps 0, 1, 2, 12 only
+    print(f'== mlp_bwd_ens_kernel (fit step, {"split" if split else "paired"} heads + NLL upstream): {nb} workgroups')
+    phases = (((0, 1, 'NLL upstream'), (1, 2, 'head backward'), (2, 12, 'trunk share backward')) if split else
+              ((0, 5, ' start -> NLL loop'), (5, 6, ' NLL element loop'), (6, 7, ' mse wave sums'),
+               (7, 1, ' partials + barrier'), (0, 1, 'NLL upstream'), (1, 2, 'heads out bwd'),
+               (2, 3, 'hidden act grad'), (3, 4, 'heads -> trunk catK'), (4, 12, 'trunk backward')))
+    for a, b, name in phases:
         ok = (bw[:, a] > 0) & (bw[:, b] > 0)
         if ok.any():
             d = bw[ok, b] - bw[ok, a]
