@@ -186,6 +186,13 @@ class CriticHead(ctypes.Structure):
                 ('loss', P), ('loss_part', P)]
 
 
+class WgradAdam(ctypes.Structure):
+    """drpo_wgrad_adam_t"""
+    _fields_ = [('g', P), ('p', P), ('m', P), ('v', P), ('lr_over_bc1', c_float), ('bc2_sqrt', c_float),
+                ('beta1', c_float), ('beta2', c_float), ('eps', c_float), ('weight_decay', c_float),
+                ('map', P), ('map_host', P)]
+
+
 class SumDesc(ctypes.Structure):
     """drpo_sum_t"""
     _fields_ = [('part', P), ('n', c_int), ('out', P)]
@@ -205,6 +212,7 @@ PROTOTYPES.update({
     'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P, c_size_t, P]),
     'drpo_mlp_wgrad_reduce': (c_int, [POINTER(WgradItem), c_int, POINTER(EnsReduce), P, c_size_t, P]),
     'drpo_mlp_wgrad_sums': (c_int, [POINTER(WgradItem), c_int, POINTER(SumDesc), c_int, P, c_size_t, P]),
+    'drpo_mlp_wgrad_adam': (c_int, [POINTER(WgradItem), c_int, P, POINTER(WgradAdam), P, c_size_t, P]),
     'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
                                   c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
     'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,

@@ -115,6 +115,25 @@ __device__ __forceinline__ float fast_tanh(float x) {        // 1 - 2 / (exp(2x)
 }
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
 
+__device__ __forceinline__ float torch_lerp(float s, float e, float w) {
+  // at::native lerp: w < 0.5 ? s + w*(e-s) : e - (e-s)*(1-w)
+  return (fabsf(w) < 0.5f) ? fmaf(w, e - s, s) : fmaf(-(e - s), 1.f - w, e);
+}
+
+// torch.optim.Adam's single-tensor step for one element (coupled L2 weight decay),
+// shared by the fused optimizer launch and the weight-gradient launch's fused step so
+// both round identically. Opt: any descriptor with lr_over_bc1, bc2_sqrt, beta1,
+// beta2, eps, weight_decay (drpo_optim_seg_t, drpo_wgrad_adam_t).
+template <typename Opt>
+__device__ __forceinline__ void adam_step(const Opt& S, float coef, float g, float& p, float& m, float& v) {
+  float ge = g * coef;
+  if (S.weight_decay != 0.f) ge = fmaf(p, S.weight_decay, ge);
+  m = torch_lerp(m, ge, 1.f - S.beta1);
+  v = fmaf(v, S.beta2, (1.f - S.beta2) * ge * ge);
+  const float denom = sqrtf(v) / S.bc2_sqrt + S.eps;
+  p = p - S.lr_over_bc1 * (m / denom);
+}
+
 // ---------------------------------------------------------------------------
 // Philox4x32-10
 // ---------------------------------------------------------------------------

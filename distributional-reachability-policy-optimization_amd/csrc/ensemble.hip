@@ -242,7 +242,9 @@ __global__ __launch_bounds__(256) void ens_loss_kernel(const float* __restrict__
 
 // per-member NLL, total loss, bound gradients from the block partials
 // (ens_reduce.hpp; also run as the last block of a drpo_mlp_wgrad_reduce launch)
-__global__ __launch_bounds__(256) void ens_loss_reduce_kernel(drpo_ens_reduce_t r) { ens_loss_reduce_block(r); }
+__global__ __launch_bounds__(256) void ens_loss_reduce_kernel(drpo_ens_reduce_t r) {
+  ens_loss_reduce_block(r, (const drpo_wgrad_adam_t*)nullptr);
+}
 
 // rows per loss workgroup: one row per thread (256 / KP rows of KP column lanes)
 static int loss_rows(int S1);

@@ -58,11 +58,6 @@ struct AdamArgs {
   const float* lr_scale;  // optional device scalar multiplying the step (nullptr = 1)
 };
 
-__device__ __forceinline__ float torch_lerp(float s, float e, float w) {
-  // at::native lerp: w < 0.5 ? s + w*(e-s) : e - (e-s)*(1-w)
-  return (fabsf(w) < 0.5f) ? fmaf(w, e - s, s) : fmaf(-(e - s), 1.f - w, e);
-}
-
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   __shared__ float s_coef;
   if (a.partial) {
@@ -299,12 +294,7 @@ __device__ __forceinline__ void pack_write4(const drpo_pack_map_t* mp, int64_t i
 // per-element update shared by both task kinds: g (already scaled) -> Adam on p, m, v
 __device__ __forceinline__ void adam_elem(const drpo_optim_seg_t& S, float coef, float g, float& p, float& m,
                                           float& v) {
-  float ge = g * coef;
-  if (S.weight_decay != 0.f) ge = fmaf(p, S.weight_decay, ge);
-  m = torch_lerp(m, ge, 1.f - S.beta1);
-  v = fmaf(v, S.beta2, (1.f - S.beta2) * ge * ge);
-  const float denom = sqrtf(v) / S.bc2_sqrt + S.eps;
-  p = p - S.lr_over_bc1 * (m / denom);
+  adam_step(S, coef, g, p, m, v);
 }
 
 // EMA of one target element (one explicit fma: both task kinds round alike)

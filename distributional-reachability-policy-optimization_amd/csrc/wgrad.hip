@@ -75,6 +75,7 @@ struct WgradPlan {
   int chunk;               // rows per chunk (multiple of WG_ROWQ)
   int va, vb;              // 16-byte loads of dZ / Y rows (widths % 4 == 0, aligned)
   int z2;                  // a second dZ term (item dz2)
+  int pk_layer;            // fused Adam: the item's matrix in the pack map (-1: none)
   int64_t first_unit;      // first logical workgroup of the item
   int64_t first_tile;      // first arrival counter of the item
   int64_t slab_off;        // first slab float of the item (tiles with nch > 1)
@@ -82,7 +83,7 @@ struct WgradPlan {
 
 constexpr int WG_MAXSUMS = 4;
 
-struct WgradArgs {
+struct WgradArgs {   // (kernarg: <= 4 KB, static_assert below)
   int64_t first[WG_MAXITEMS];        // first logical workgroup per item (unused: INT64_MAX)
   drpo_wgrad_item_t it[WG_MAXITEMS];
   WgradPlan pl[WG_MAXITEMS];
@@ -92,6 +93,8 @@ struct WgradArgs {
   drpo_ens_reduce_t red;
   int nsums;                         // > 0: one extra (logically last) block adds partial sums
   drpo_sum_t sums[WG_MAXSUMS];
+  int has_adam;                      // fused Adam step (drpo_mlp_wgrad_adam)
+  drpo_wgrad_adam_t adam;
   float* slab;
   unsigned* ctr;
 };
@@ -331,14 +334,31 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
   float gv[E];
   const bool bias_mine = do_bias && tid < TO && o0 + tid < dout;
   float gbv = 0.f;
+  // fused Adam (drpo_mlp_wgrad_adam): the parameters and moments of the tile, loaded with
+  // the gradient's current values
+  const bool adam = a.has_adam;
+  const int64_t eW = adam ? gW - a.adam.g : 0, eb = adam ? gb - a.adam.g : 0;   // flat element offsets
+  float ap[E], am[E], av[E], bp = 0.f, bm = 0.f, bvv = 0.f;
   auto load_grad = [&]() {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int idx = tid + WG_NT * e;
       const int o = o0 + idx / TI, i = i0 + idx % TI;
-      gv[e] = (o < dout && i < din) ? gW[(size_t)o * din + i] : 0.f;
+      const bool in = o < dout && i < din;
+      const int64_t k = (int64_t)o * din + i;
+      gv[e] = in ? gW[k] : 0.f;
+      if (adam) {
+        ap[e] = in ? a.adam.p[eW + k] : 0.f;
+        am[e] = in ? a.adam.m[eW + k] : 0.f;
+        av[e] = in ? a.adam.v[eW + k] : 0.f;
+      }
     }
     gbv = bias_mine ? gb[o0 + tid] : 0.f;
+    if (adam && bias_mine) {
+      bp = a.adam.p[eb + o0 + tid];
+      bm = a.adam.m[eb + o0 + tid];
+      bvv = a.adam.v[eb + o0 + tid];
+    }
   };
   if (P.nch > 1) {
     float* my = a.slab + P.slab_off + (tile_local * P.nch + ch) * SL;
@@ -387,6 +407,43 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
     }
   } else {
     load_grad();
+  }
+  if (adam) {
+    // the finished gradient g = current terms + this launch's sum -> Adam (the
+    // drpo_optim_step arithmetic), the tile's forward / transposed mirrors refreshed; the
+    // gradient itself is never written (nonzero input terms are cleared)
+    const drpo_pack_map_t* md = P.pk_layer >= 0 ? (const drpo_pack_map_t*)a.adam.map : nullptr;
+    const int ncb = (dout + 15) >> 4, nks = (din + 15) >> 4;
+    const int64_t mb = md ? md->poff[P.pk_layer] + (int64_t)zb * ncb * nks * 256 : 0;
+    float* PM = md ? md->P : nullptr;
+    float* PTM = md ? md->PT : nullptr;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int idx = tid + WG_NT * e;
+      const int o = o0 + idx / TI, i = i0 + idx % TI;
+      if (o < dout && i < din) {
+        const int64_t k = (int64_t)o * din + i;
+        float pe = ap[e], me = am[e], ve = av[e];
+        adam_step(a.adam, 1.f, gv[e] + pv[e], pe, me, ve);
+        a.adam.p[eW + k] = pe;
+        a.adam.m[eW + k] = me;
+        a.adam.v[eW + k] = ve;
+        if (gv[e] != 0.f) gW[k] = 0.f;
+        if (PM)   // forward mirror: fragment (o>>4, i>>4), lane ((i>>2)&3)*16 + (o&15), component i&3
+          PM[mb + ((int64_t)((o >> 4) * nks + (i >> 4)) << 8) + ((((i >> 2) & 3) * 16 + (o & 15)) << 2) + (i & 3)] = pe;
+        if (PTM)  // transposed: fragment (i>>4, o>>4), lane ((o>>2)&3)*16 + (i&15), component o&3
+          PTM[mb + ((int64_t)((i >> 4) * ncb + (o >> 4)) << 8) + ((((o >> 2) & 3) * 16 + (i & 15)) << 2) + (o & 3)] = pe;
+      }
+    }
+    if (bias_mine) {
+      adam_step(a.adam, 1.f, gbv + pb, bp, bm, bvv);
+      a.adam.p[eb + o0 + tid] = bp;
+      a.adam.m[eb + o0 + tid] = bm;
+      a.adam.v[eb + o0 + tid] = bvv;
+      if (gbv != 0.f) gb[o0 + tid] = 0.f;
+    }
+    STAMPG(4);
+    return;
   }
   // gradient += sum (the caller's gradient is zeroed or holds terms to accumulate)
   float sq = 0.f;
@@ -437,7 +494,10 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs args) {
   STAMPG(0);
   const int64_t bid = xcd_block().x;
   if (bid >= a.units) {        // the extra blocks: deferred reductions
-    if (a.has_red && bid == a.units) ens_loss_reduce_block(a.red);
+    if (a.has_red && bid == a.units) {
+      typedef const __attribute__((address_space(4))) drpo_wgrad_adam_t AdamK;
+      ens_loss_reduce_block(a.red, a.has_adam ? &a.adam : (AdamK*)nullptr);
+    }
     else if (a.nsums) sums_block(a, wsm);
     return;
   }
@@ -453,6 +513,8 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs args) {
   else if (P.ti == 64) wgrad_unit_v<16, 64>(a, q, u, wsm);
   else wgrad_unit_v<16, 16>(a, q, u, wsm);
 }
+
+static_assert(sizeof(WgradArgs) <= 4096, "weight-gradient kernarg");
 
 // LDS: 4 wave slabs of the largest tile + bias partials + the block-sum scratch
 static size_t wgrad_lds() { return sizeof(float) * ((size_t)WG_NW * 16 * WG_SLD + WG_NW * 64 + 8); }
@@ -590,7 +652,19 @@ DRPO_API int drpo_mlp_wgrad(const drpo_wgrad_item_t* items, int n, void* workspa
 }
 
 static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, const drpo_sum_t* sums,
-                        int nsums, void* workspace, size_t workspace_bytes, hipStream_t stream);
+                        int nsums, void* workspace, size_t workspace_bytes, hipStream_t stream,
+                        const drpo_wgrad_adam_t* adam = nullptr);
+
+DRPO_API int drpo_mlp_wgrad_adam(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red,
+                                 const drpo_wgrad_adam_t* adam, void* workspace, size_t workspace_bytes,
+                                 drpo_stream_t stream_) {
+  DRPO_REQUIRE(adam && adam->g && adam->p && adam->m && adam->v && adam->bc2_sqrt > 0.f &&
+                   (!adam->map == !adam->map_host),
+               "drpo_mlp_wgrad_adam: bad Adam descriptor (g, p, m, v; map with its host copy)");
+  for (int k = 0; k < n; ++k)
+    DRPO_REQUIRE(!items[k].sq, "drpo_mlp_wgrad_adam: item %d asks for clip partials (no clip in the fused step)", k);
+  return wgrad_launch(items, n, red, nullptr, 0, workspace, workspace_bytes, (hipStream_t)stream_, adam);
+}
 
 DRPO_API int drpo_mlp_wgrad_reduce(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red,
                                    void* workspace, size_t workspace_bytes, drpo_stream_t stream_) {
@@ -607,7 +681,8 @@ DRPO_API int drpo_mlp_wgrad_sums(const drpo_wgrad_item_t* items, int n, const dr
 }
 
 static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, const drpo_sum_t* sums,
-                        int nsums, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+                        int nsums, void* workspace, size_t workspace_bytes, hipStream_t stream,
+                        const drpo_wgrad_adam_t* adam) {
   DRPO_REQUIRE(n >= 0 && n <= WG_MAXITEMS && (n == 0 || items), "drpo_mlp_wgrad: at most %d items", WG_MAXITEMS);
   static Plan p;   // host scratch (the library is driven by one host thread per process)
   const int rc = plan(items, n, red, p);
@@ -619,6 +694,22 @@ static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_re
   p.a.slab = (float*)((char*)workspace + (size_t)((p.tiles * 4 + 255) / 256 * 256));
   p.a.nsums = nsums;
   for (int q = 0; q < nsums; ++q) p.a.sums[q] = sums[q];
+  p.a.has_adam = adam != nullptr;
+  if (adam) {
+    p.a.adam = *adam;
+    // each item's matrix in the group's pack map (by its flat offset), for the mirrors
+    const drpo_pack_map_t* mh = (const drpo_pack_map_t*)adam->map_host;
+    for (int k = 0; k < p.a.n; ++k) {
+      const drpo_wgrad_item_t& I = p.a.it[k];
+      p.a.pl[k].pk_layer = -1;
+      if (!mh) continue;
+      const int64_t off = I.gW - adam->g;
+      for (int l = 0; l < mh->nlayers && l < 16; ++l)
+        if (mh->off[l] == off && mh->din[l] == I.din && mh->dout[l] == I.dout && mh->nbatch[l] == I.nbatch)
+          p.a.pl[k].pk_layer = l;
+      DRPO_REQUIRE(p.a.pl[k].pk_layer >= 0, "drpo_mlp_wgrad_adam: item %d is not a matrix of the pack map", k);
+    }
+  }
   const int64_t blocks = p.a.units + (red ? 1 : 0) + (nsums ? 1 : 0);
   if (blocks == 0) return DRPO_OK;
   mlp_wgrad_kernel<<<(unsigned)blocks, WG_NT, wgrad_lds(), stream>>>(p.a);

@@ -57,6 +57,10 @@ def split_heads_bwd(n, Z):
 class EnsembleEngine:
     def __init__(self, model):
         self.m = model
+        # single-process fit: Adam (+ mirror refresh) fused into the weight-gradient launch
+        # (drpo_mlp_wgrad_adam; bitwise the same step as drpo_optim_step). DRPO_FIT_FUSED_ADAM=0
+        # keeps the separate optimizer launch (A/B).
+        self.fused_adam = os.environ.get('DRPO_FIT_FUSED_ADAM', '1') != '0'
         self.ws = {}
         self.wg_ws = {}
         self.noise = None
@@ -396,6 +400,20 @@ class EnsembleEngine:
             draws = [np.asarray(nz.randint(n, full))[z0 * b:z0 * b + rows] for _ in range(steps)]
             idx_all = torch.from_numpy(np.ascontiguousarray(np.stack(draws), dtype=np.int64)).to(self.dev)
         stream = _lib.stream()
+        # Adam fused into the weight-gradient launch: single process, whole group, no clip
+        fuse = self.fused_adam and fused and sh is None and not self.dp.active and len(wl) == 1
+        if fuse:
+            from ._abi import WgradAdam
+            opt = m.optimizer
+            opt._ensure_state()
+            pm = g.pack_map()
+            ad = WgradAdam()
+            ad.g, ad.p, ad.m, ad.v = g.grad.data_ptr(), g.data.data_ptr(), opt.m.data_ptr(), opt.v.data_ptr()
+            ad.beta1, ad.beta2 = opt.betas
+            ad.eps, ad.weight_decay = opt.eps, opt.weight_decay
+            ad.map, ad.map_host = pm.data_ptr(), ctypes.addressof(pm.host)
+            warr, wn = wl[0]
+            wws = self._wgrad_ws('fit0', warr, wn)
         gargs = [_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states), _lib.ptr(rb._rewards),
                  ptr_host, _lib.ptr(ptr_dev), rb.capacity, rows]
         loss_base = losses.data_ptr()
@@ -430,6 +448,12 @@ class EnsembleEngine:
                     ctypes.c_void_p(red_in.loss)
                 _lib.check(L.drpo_ens_loss_partials(*largs, ctypes.byref(red), stream), 'ens_loss')
                 _lib.check(L.drpo_mlp_backward(ctypes.byref(bd), stream), 'ensemble backward')
+            if fuse:
+                # weight gradients + the NLL reduction + Adam + mirror refresh: one launch
+                ad.lr_over_bc1, ad.bc2_sqrt = m.optimizer.step_scalars()
+                _lib.check(L.drpo_mlp_wgrad_adam(warr, wn, ctypes.byref(red), ctypes.byref(ad), wws.data_ptr(),
+                                                 wws.numel(), stream), 'ensemble wgrad + adam')
+                continue
             # the loss reduction rides as the last workgroup of the wgrad launch
             self._wgrad('fit', wl, red, stream)
             if sh is None:

@@ -352,6 +352,26 @@ typedef struct {
 int drpo_mlp_wgrad_sums(const drpo_wgrad_item_t* items /* host */, int n, const drpo_sum_t* sums /* host */,
                         int nsums, void* workspace, size_t workspace_bytes, drpo_stream_t stream);
 
+/* The Adam step fused into the weight-gradient launch (no clip, no data-parallel
+ * exchange between the gradient and the step: the single-process model fit,
+ * src/dynamics.py:155-183 with torch.optim.Adam): the workgroup that finishes an output
+ * tile applies Adam to it (the drpo_optim_step arithmetic, so results are bitwise
+ * those of drpo_mlp_wgrad + drpo_optim_step) and refreshes the tile's packed mirrors;
+ * the optional reduction block does the same for the log-var bounds. The gradient
+ * buffer is consumed without being written (it must hold zeros or terms to add; any
+ * nonzero term is cleared, like drpo_optim_step's zero_grad). */
+struct drpo_pack_map_s;
+typedef struct {
+  const float* g;             /* base of the flat gradient the items' gW / gb (and gmin / gmax) point into */
+  float *p, *m, *v;           /* the group's data and Adam moments, indexed like g */
+  float lr_over_bc1, bc2_sqrt, beta1, beta2, eps, weight_decay;
+  const struct drpo_pack_map_s* map;      /* device pack map of the group (mirrors refreshed) or NULL */
+  const struct drpo_pack_map_s* map_host; /* its host copy (which matrix each item is) */
+} drpo_wgrad_adam_t;
+int drpo_mlp_wgrad_adam(const drpo_wgrad_item_t* items /* host */, int n, const drpo_ens_reduce_t* red /* host or NULL */,
+                        const drpo_wgrad_adam_t* adam /* host */, void* workspace, size_t workspace_bytes,
+                        drpo_stream_t stream);
+
 /* ---------------------------------------------------------------- packed weight mirrors
  * Every MLP kernel streams weights from fragment-linear mirrors of the PyTorch
  * [nbatch][dout][din] tensors (layout: csrc/pack.hip). The mirrors are refreshed
@@ -486,7 +506,7 @@ int drpo_ema(float* target, const float* source, int64_t n, float rate, drpo_str
  * partial sums (clip_grad_norm_, src/ssac.py:450-451), Adam (src/defaults.py:4),
  * gradient zeroing, EMA of a target group (src/torch_util.py:223-226) and the
  * packed-mirror refresh, in ONE launch.                                        */
-typedef struct {              /* device memory: where each weight matrix of a group lives */
+typedef struct drpo_pack_map_s { /* device memory: where each weight matrix of a group lives */
   int nlayers;
   int64_t off[16];            /* flat offset of the [nbatch][dout][din] weight */
   int din[16], dout[16], nbatch[16];

@@ -379,3 +379,53 @@ def test_config_rollout_teacher_forced_dying_rows(c):
     assert off == n and steps <= H
     assert marginal_total <= 4, marginal_total
     print(f'config {c}: {n} rows over {steps} steps, {checked} teacher-forced rows checked')
+
+
+@pytest.mark.parametrize('c', [2])
+def test_fit_fused_adam_matches_separate_step(c):
+    """The fit's Adam fused into the weight-gradient launch (drpo_mlp_wgrad_adam) against
+    the separate drpo_optim_step launch, both on the split-heads backward: the same
+    per-element arithmetic, so parameters, Adam moments and both packed mirrors are
+    bitwise equal after 3 production-noise steps. The paired backward (one workgroup per
+    row tile, trunk dZ by the concatenated-K product) differs only in summation order."""
+    from drpo_amd.rng import DeviceNoise
+    alg, cd = _alg(c, B=256)
+    m = alg.model_ensemble
+    eng = m.engine
+    _fill(alg, cd['env'], 30000, 7)
+    g = m.group
+    m.optimizer._ensure_state()
+    start = [g.data.clone(), m.optimizer.m.clone(), m.optimizer.v.clone(), m.optimizer.step_count]
+
+    def run(fused, split):
+        g.data.copy_(start[0])
+        m.optimizer.m.copy_(start[1])
+        m.optimizer.v.copy_(start[2])
+        m.optimizer.step_count = start[3]
+        g.mark_dirty()
+        g.ensure_packed()
+        eng.fused_adam = fused
+        import os
+        os.environ['DRPO_SPLIT_BWD'] = '1' if split else '0'
+        eng.ws.clear()
+        eng.wg_ws.clear()
+        losses = m.fit(alg.replay_buffer, steps=3, noise=DeviceNoise(1234))
+        torch.cuda.synchronize()
+        out = [g.data.clone(), m.optimizer.m.clone(), m.optimizer.v.clone(), g.packed.clone(), g.packedT.clone(),
+               g.grad.clone()]
+        return losses, out
+
+    try:
+        l_f, o_f = run(True, True)
+        l_s, o_s = run(False, True)
+        l_p, o_p = run(False, False)
+    finally:
+        import os
+        os.environ.pop('DRPO_SPLIT_BWD', None)
+        eng.fused_adam = True
+    assert l_f == l_s
+    for a, b, what in zip(o_f, o_s, ['data', 'm', 'v', 'packed', 'packedT', 'grad']):
+        assert torch.equal(a, b), what
+    assert int((o_f[5] != 0).sum()) == 0           # the gradient is left zeroed
+    np.testing.assert_allclose(l_p, l_f, rtol=1e-5)
+    _close(o_p[0], o_f[0].cpu().numpy(), 2e-5, 'paired vs split backward: parameters')
