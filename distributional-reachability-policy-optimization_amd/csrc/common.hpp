@@ -546,6 +546,54 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
   tile_dense_nc<NW, RB, MAXC, ACT, NK, NL>(nc, in, ldi, K, P, bias, N, out, ldo, gs, Pl);
 }
 
+// 200-wide layer with K = 200 (13 column blocks x 13 k-steps) on 8 waves, balanced over
+// the 4 SIMDs (wave w runs on SIMD w % 4): waves 0-3 own blocks w and w + 8, waves 4-7
+// own block w plus a quarter of block 12's k-steps (4 / 3 / 3 / 3). Each SIMD then
+// issues 3.25 blocks of MFMAs instead of 4 on SIMD 0 and 3 on the others. Block 12's
+// partial tiles go to red[4][256]; after the caller's barrier tile_dense_13s_finish
+// sums them (fixed order), adds the bias and applies the activation. Returns the bias
+// value that thread (< 256) needs for the finish.
+template <int ACT>
+__device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const float* __restrict__ P,
+                                                const float* __restrict__ bias, float* out, int ldo, float* red) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  if (wave < 4) {
+    const int col = 192 + (threadIdx.x & 15);
+    const float b12 = col < 200 ? gload(bias + col) : 0.f;
+    tile_dense_core<8, 1, 2, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
+    return b12;
+  }
+  const int q = wave - 4;
+  const int ks0 = q == 0 ? 0 : 1 + 3 * q, nks = q == 0 ? 4 : 3;
+  f32x4 bq[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) bq[u] = load_pk(P, 12, ks0 + (u < nks ? u : nks - 1), 13);
+  tile_dense_core<8, 1, 1, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (u < nks) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(in + l15 * ldi + 16 * (ks0 + u) + 4 * g);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], bq[u][m], acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[q * 256 + (4 * g + r) * 16 + l15] = acc[r];
+  return 0.f;
+}
+
+template <int ACT>
+__device__ __forceinline__ void tile_dense_13s_finish(const float* red, float b12, float* out, int ldo) {
+  const int tid = threadIdx.x;
+  if (tid < 256) {
+    const int r = tid >> 4, c = tid & 15;
+    const float z = ((red[tid] + red[256 + tid]) + (red[512 + tid] + red[768 + tid])) + b12;
+    out[r * ldo + 192 + c] = 192 + c < 200 ? act_fn<ACT>(z) : 0.f;
+  }
+}
+
 // K (input width) -> compile-time k-step count for the widths on the path
 // (<= 16 inputs -> 1 step, 49..64 -> 4, 200 -> 13, 256 -> 16), else the runtime loop.
 template <int NW, int RB, int MAXC, int ACT>

@@ -685,6 +685,9 @@ __device__ __forceinline__ void persist_noise(const float* eps_a, const float* e
 // each step, and the layers run at the CU's L2 read rate). Needs S <= 16,
 // Ha == 256, 2A <= 16 and the LDS to spare (host check).
 constexpr int PERSIST_L2_LDS = 3;
+#ifndef DRPO_M2_SPLIT
+#define DRPO_M2_SPLIT 1   // A/B macro: the member hidden layer split over K for SIMD balance
+#endif
 
 // PM: the dynamics heads' path fixed at compile time (1: paired heads, S+1 <= 16 and
 // Hm = 200; 0: the general path; -1: chosen at run time), so a specialised kernel holds
@@ -873,6 +876,14 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     tile_dense<NW, RB, MAXC, ACT_SILU>(xin, ldx, S + A, MW(mW1, ms_in), MB(mb1, Hm), Hm, h1, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(5);
+#if DRPO_M2_SPLIT
+    if (RB == 1 && NW == 8 && Hm == 200) {
+      // member hidden layer balanced over the SIMDs (13th block split over K)
+      const float b12 = tile_dense_13s<ACT_SILU>(h1, ldh, MW(mW2, ms_hid), MB(mb2, Hm), h2, ldh, red);
+      lds_barrier();
+      tile_dense_13s_finish<ACT_SILU>(red, b12, h2, ldh);
+    } else
+#endif
     tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, MW(mW2, ms_hid), MB(mb2, Hm), Hm, h2, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(6);
