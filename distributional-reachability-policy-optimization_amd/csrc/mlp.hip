@@ -326,6 +326,22 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
     float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
     outp = nullptr;
     heads_pair<RB>(a, t, T, t == bA ? bB : bA, xin, z, row0, nrows, red);
+    if (a->ccb_out) {
+      // the constraint critic's upper bound, max over C (drpo_cc_head), from the heads'
+      // outputs in LDS (mean head: xin columns 0.., log-std head: columns 16..)
+      lds_barrier();
+      if (tid < nrows) {
+        const int C = a->net[1].L[1].dout;
+        const float* rowp = xin + tid * LDH;
+        float best = 0.f;
+        for (int c = 0; c < C; ++c) {
+          float v = rowp[c];
+          if (a->ccb_dist) v = v + a->ccb_ratio * cc_std(rowp[16 + c], a->ccb_lmin, a->ccb_lmax);
+          if (c == 0 || v > best) best = v;
+        }
+        a->ccb_out[(size_t)z * a->rows + row0 + tid] = best;
+      }
+    }
   } else {
     float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
     const int w = a->net[0].L[a->net[0].nl - 1].dout;
@@ -377,6 +393,13 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
     if (a->head.mode != 0)
       DRPO_REQUIRE(a->head.mode <= 3 && a->head.A >= 1 && 2 * a->head.A == a->net[0].L[a->net[0].nl - 1].dout,
                    "drpo_mlp_forward_multi: job %d policy head shape", j);
+    if (a->ccb_out) {   // the same conditions as heads_pairable (device side)
+      const drpo_mlp_net_t &n1 = a->net[1], &n2 = a->net[2];
+      DRPO_REQUIRE(a->trunk && a->nnets == 3 && n1.nl == 2 && n2.nl == 2 && n1.L[0].din == 256 &&
+                       n2.L[0].din == 256 && n1.L[0].dout == n2.L[0].dout && n1.L[0].act == n2.L[0].act &&
+                       n1.L[1].act == n2.L[1].act && n1.L[1].dout <= 16 && n2.L[1].dout <= 16,
+                   "drpo_mlp_forward_multi: job %d: the constraint bound needs a trunk job with paired heads", j);
+    }
     const int ns = a->trunk ? 1 : a->nnets;
     DRPO_REQUIRE(slots + ns <= MJ_MAXSLOT, "drpo_mlp_forward_multi: too many nets");
     for (int h = 0; h < ns; ++h) {

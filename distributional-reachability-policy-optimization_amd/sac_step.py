@@ -462,11 +462,13 @@ class SACEngine:
         _lib.check(L.drpo_policy_head(raw.data_ptr(), self.B, self.A, mode, _p(eps), seed, ctr, site, _p(a), _p(logp),
                                       _p(u), _p(e), _p(amean), _lib.stream()), 'policy_head')
 
-    def _cc_head(self, mu, ls, ubmax, dist):
+    def _ccb(self, d, out, dist):
+        """The constraint critic's max-C upper bound (drpo_cc_head's arithmetic) formed
+        by the multi-job forward from the paired heads' outputs (drpo_mlp_fwd_t.ccb_*)."""
         cc = self.sol.constraint_critic
-        _lib.check(_lib.lib().drpo_cc_head(mu.data_ptr(), ls.data_ptr(), self.B, self.C, int(dist), float(cc.std_ratio),
-                                           float(cc.log_std_min), float(cc.log_std_max), ubmax.data_ptr(), None,
-                                           _lib.stream()), 'cc_head')
+        d.ccb_out, d.ccb_dist = out.data_ptr(), int(dist)
+        d.ccb_ratio, d.ccb_lmin, d.ccb_lmax = float(cc.std_ratio), float(cc.log_std_min), float(cc.log_std_max)
+        return d
 
     def _clean_grads(self, group):
         """Gradients must be zero before the backward passes accumulate into them; the
@@ -671,12 +673,12 @@ class SACEngine:
             fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
             fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True),
             fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)] + ([
-            fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True)] if mlp_mult else []),
-            ctr)
+            self._ccb(fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True),
+                      self.buf('a.sqc', B), dist)] if mlp_mult else []), ctr)
         if mlp_mult:
-            # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad)
+            # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad); the bound is formed
+            # by the forward launch above
             sqc = self.buf('a.sqc', B)
-            self._cc_head(ws['a.ccm.mu'], ws['a.ccm.ls'], sqc, dist)
             self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
                                                      [(self.bs, S), (sqc, 1), (None, 0)], B))
         # The actor losses' output gradients are formed inside the two backward launches
@@ -825,12 +827,11 @@ class SACEngine:
             with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A, None,
                       0, amean=am)], ctr)
         # launch 2: constraint critic at (s, a) and at (s, tanh(mu_safe))
-        self._run_multi('m.f2', lambda: [
-            fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
-            fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True)], ctr)
         aqc, sqc = self.buf('m.aqc', B), self.buf('m.sqc', B)
-        self._cc_head(ws['m.cc.mu'], ws['m.cc.ls'], aqc, dist)
-        self._cc_head(ws['m.ccs.mu'], ws['m.ccs.ls'], sqc, dist)
+        self._run_multi('m.f2', lambda: [
+            self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc, dist),
+            self._ccb(fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True), sqc,
+                      dist)], ctr)
         xm = self.buf('m.x', B, S + 1)
         self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B, save_x=xm))
         gx = self.buf('m.gx', B)
@@ -873,10 +874,10 @@ class SACEngine:
         self._run_multi('m.f1s' + noise_tag(e7), lambda: [
             with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A,
                       e7, SITE_PI_MULT, a=a)], ctr)
-        self._run_multi('m.f2s', lambda: [
-            fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True)], ctr)
         aqc = self.buf('m.aqc', B)
-        self._cc_head(ws['m.cc.mu'], ws['m.cc.ls'], aqc, dist)
+        self._run_multi('m.f2s', lambda: [
+            self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc,
+                      dist)], ctr)
         psum = self._loss_slots(1)
         _lib.check(L.drpo_multiplier_head(B, None, None, aqc.data_ptr(), float(sol.constraint_threshold),
                                           float(sol.penalty_lb), float(sol.penalty_ub), 0.0, 0.0, None,

@@ -162,6 +162,13 @@ typedef struct {
   int split_heads;     /* trunk mode, single launches: one workgroup per (row tile, head); each
                           recomputes the trunk (only head 1's workgroup saves it) -- twice the
                           workgroups for small ensembles (fit: 16 tiles x 7 members) */
+  float* ccb_out;      /* multi-job launches, trunk job with paired heads (the constraint critic,
+                          src/ssac.py:46-92): per-row max over the C constraints of the quantile
+                          bound mu + ccb_ratio * std(log-std raw) (ccb_dist) or of mu, formed from
+                          the heads' outputs in the launch (drpo_cc_head's arithmetic,
+                          src/ssac.py:474-494,536-560); NULL: none */
+  int ccb_dist;
+  float ccb_ratio, ccb_lmin, ccb_lmax;
 } drpo_mlp_fwd_t;
 
 typedef struct {
