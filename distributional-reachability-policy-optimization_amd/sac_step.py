@@ -462,13 +462,34 @@ class SACEngine:
         _lib.check(L.drpo_policy_head(raw.data_ptr(), self.B, self.A, mode, _p(eps), seed, ctr, site, _p(a), _p(logp),
                                       _p(u), _p(e), _p(amean), _lib.stream()), 'policy_head')
 
+    def _ccb_fused(self):
+        """The multi-job forward can form the bound when the constraint critic's heads are
+        pairable (256-wide trunk, two [256 -> H -> C <= 16] heads: the reference widths)."""
+        t, h1, h2 = self._cc_nets()
+        (_, _, _, tw, _, _), l1, l2 = t.layers[-1], h1.layers, h2.layers
+        return (tw == 256 and len(l1) == 2 and len(l2) == 2 and l1[0][3] == l2[0][3] and l1[1][3] <= 16
+                and l2[1][3] <= 16 and l1[0][4] == l2[0][4] and l1[1][4] == l2[1][4])
+
     def _ccb(self, d, out, dist):
         """The constraint critic's max-C upper bound (drpo_cc_head's arithmetic) formed
-        by the multi-job forward from the paired heads' outputs (drpo_mlp_fwd_t.ccb_*)."""
+        by the multi-job forward from the paired heads' outputs (drpo_mlp_fwd_t.ccb_*);
+        other head shapes keep the drpo_cc_head launch (_cc_bound_after)."""
+        if not self._ccb_fused():
+            return d
         cc = self.sol.constraint_critic
         d.ccb_out, d.ccb_dist = out.data_ptr(), int(dist)
         d.ccb_ratio, d.ccb_lmin, d.ccb_lmax = float(cc.std_ratio), float(cc.log_std_min), float(cc.log_std_max)
         return d
+
+    def _cc_bound_after(self, name, out, dist):
+        """drpo_cc_head over the saved head outputs of job `name` when _ccb could not fuse it."""
+        if self._ccb_fused():
+            return
+        cc = self.sol.constraint_critic
+        mu, ls = self.ws[f'{name}.mu'], self.ws[f'{name}.ls']
+        _lib.check(_lib.lib().drpo_cc_head(mu.data_ptr(), ls.data_ptr(), self.B, self.C, int(dist), float(cc.std_ratio),
+                                           float(cc.log_std_min), float(cc.log_std_max), out.data_ptr(), None,
+                                           _lib.stream()), 'cc_head')
 
     def _clean_grads(self, group):
         """Gradients must be zero before the backward passes accumulate into them; the
@@ -679,6 +700,7 @@ class SACEngine:
             # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad); the bound is formed
             # by the forward launch above
             sqc = self.buf('a.sqc', B)
+            self._cc_bound_after('a.ccm', sqc, dist)
             self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
                                                      [(self.bs, S), (sqc, 1), (None, 0)], B))
         # The actor losses' output gradients are formed inside the two backward launches
@@ -832,6 +854,8 @@ class SACEngine:
             self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc, dist),
             self._ccb(fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True), sqc,
                       dist)], ctr)
+        self._cc_bound_after('m.cc', aqc, dist)
+        self._cc_bound_after('m.ccs', sqc, dist)
         xm = self.buf('m.x', B, S + 1)
         self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B, save_x=xm))
         gx = self.buf('m.gx', B)
@@ -878,6 +902,7 @@ class SACEngine:
         self._run_multi('m.f2s', lambda: [
             self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc,
                       dist)], ctr)
+        self._cc_bound_after('m.cc', aqc, dist)
         psum = self._loss_slots(1)
         _lib.check(L.drpo_multiplier_head(B, None, None, aqc.data_ptr(), float(sol.constraint_threshold),
                                           float(sol.penalty_lb), float(sol.penalty_ub), 0.0, 0.0, None,
