@@ -574,11 +574,17 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     return v >= 1 && v <= 64 ? v : 2;
   }();
   const int64_t slots = per_cu * (int64_t)wg_cus();
+  static const double min_rows = [] {   // A/B knob: minimum rows per unit (profiles/wgrad_probe.py)
+    const char* e = getenv("DRPO_WGRAD_MIN_ROWS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? (double)v : 0.0;
+  }();
   auto units_for = [&](double per, int* nch, int* chunk) {
     int64_t tot = 0;
     for (int k = 0; k < m; ++k) {
       const Shape& s = sh[k];
-      const double rows_per = per * 16.0 / kg_cost(s.to, s.ti);   // rows whose cost per wave is `per`
+      double rows_per = per * 16.0 / kg_cost(s.to, s.ti);   // rows whose cost per wave is `per`
+      if (rows_per < min_rows) rows_per = min_rows;              // a unit's fixed costs need work to amortise
       int64_t c = (int64_t)((double)s.rows / (rows_per > 1 ? rows_per : 1) + 0.5);
       c = c < 1 ? 1 : c;
       int64_t ck = (s.rows + c - 1) / c;

@@ -25,6 +25,8 @@ SA = 14      # quadrotor S + A (the input layers' width, not a multiple of 4)
 C = 2
 # the critic update's items: twin Q nets, constraint-critic trunk, mean / log-std heads
 CRITIC = [(256, SA), (256, 256), (1, 256)] * 2 + [(256, SA), (256, 256)] + [(256, 256), (C, 256)] * 2
+ACTOR = [(256, 12), (256, 256), (4, 256)] * 2          # actor + safe actor (S = 12, 2A = 4)
+MULT = [(256, 13), (256, 256), (1, 256)]               # MLPMultiplier (S + 1 inputs)
 
 
 def make(shapes, rows):
@@ -109,8 +111,9 @@ def main():
     critic = make(CRITIC, rows)
     res['critic'] = time_launch(critic, rows)
     res['critic_stamps'] = stamps(critic, rows)
-    for name, shapes in (('256x256', [(256, 256)]), ('3x256x256', [(256, 256)] * 3), ('256x16', [(256, SA)]),
-                         ('1x256', [(1, 256)])):
+    res['per_cu'] += '/min_rows=' + os.environ.get('DRPO_WGRAD_MIN_ROWS', '0')
+    for name, shapes in (('actor', ACTOR), ('mult', MULT), ('256x256', [(256, 256)]), ('3x256x256', [(256, 256)] * 3),
+                         ('256x16', [(256, SA)]), ('1x256', [(1, 256)])):
         it = make(shapes, rows)
         res[name] = time_launch(it, rows)
     print(json.dumps(res))
