@@ -80,9 +80,6 @@ ENV_JSON = {
 }
 QUAD_JSON = ENV_JSON['quadrotor']
 
-# rollout_and_update's minibatch prefetch (drpo_amd.smbpo.PREFETCH_BATCHES, same switch)
-PREFETCH = os.environ.get('DRPO_PREFETCH_BATCHES', '1') != '0'
-
 CONFIGS = {
     1: dict(env='cartpole', E=3, H=5, B=256, label='cartpole-move E=3 H=5 B=256 (BASELINE configs[0])'),
     2: dict(env='quadrotor', E=7, H=10, B=4096, label='quadrotor E=7 H=10 B=4096 (BASELINE configs[1])'),
@@ -385,8 +382,7 @@ def main():
             dlib.check(dlib.lib().drpo_event_record(tmr.events[2], dlib.stream()), 'event_record')
             if do_sac:
                 for st in range(alg.solver_updates_per_step):
-                    alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0,
-                                      prefetch_next=st + 1 < alg.solver_updates_per_step and PREFETCH)
+                    alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
             dlib.check(dlib.lib().drpo_event_record(tmr.events[3], dlib.stream()), 'event_record')
             n_dev.add_(out._count)
             return None
@@ -398,8 +394,7 @@ def main():
         t1.record()
         if do_sac:
             for st in range(alg.solver_updates_per_step):
-                alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0,
-                                  prefetch_next=st + 1 < alg.solver_updates_per_step and PREFETCH)
+                alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
         t2.record()
         n_dev.add_(out._count)            # device-side transition count (no host sync)
         return (t0, t1, t2)
@@ -458,8 +453,7 @@ def main():
         eng.profiler = LaunchProfiler()
         CommLog.timing, c0 = [], CommLog.calls      # HIP events around every gradient exchange
         for st in range(alg.solver_updates_per_step):
-            alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0,
-                              prefetch_next=st + 1 < alg.solver_updates_per_step and PREFETCH)
+            alg.update_solver(update_actor=st % 2 == 0, update_multiplier=st % 5 == 0)
         torch.cuda.synchronize()
         summ = eng.profiler.summarise()
         eng.profiler = None

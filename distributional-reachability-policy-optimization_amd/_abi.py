@@ -81,7 +81,6 @@ PROTOTYPES = {
     'drpo_event_destroy': (c_int, [P]),
     'drpo_event_record': (c_int, [P, P]),
     'drpo_event_elapsed_ms': (c_int, [POINTER(c_float), P, P]),
-    'drpo_stream_wait_event': (c_int, [P, P]),
     'drpo_grad_sumsq_blocks': (c_int, [c_int64]),
     'drpo_grad_sumsq': (c_int, [P, c_int64, P, P]),
     'drpo_adam': (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_float, c_float, P, c_int,

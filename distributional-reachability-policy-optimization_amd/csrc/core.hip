@@ -45,12 +45,6 @@ DRPO_API int drpo_event_record(void* ev, drpo_stream_t stream_) {
   return hipEventRecord((hipEvent_t)ev, stream) == hipSuccess ? DRPO_OK : DRPO_EHIP;
 }
 
-// stream waits (on the device) until the event's recorded work is done: the cross-stream
-// hand-off of the SAC minibatch prefetch (sac_step.py)
-DRPO_API int drpo_stream_wait_event(drpo_stream_t stream_, void* ev) {
-  return hipStreamWaitEvent((hipStream_t)stream_, (hipEvent_t)ev, 0) == hipSuccess ? DRPO_OK : DRPO_EHIP;
-}
-
 DRPO_API int drpo_event_elapsed_ms(float* ms, void* start, void* stop) {
   hipError_t r = hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
   if (r != hipSuccess) {

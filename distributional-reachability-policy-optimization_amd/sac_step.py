@@ -253,7 +253,6 @@ class SACEngine:
         self._actor_arena(solver.batch_size)
         self.loss_pool = None
         self.loss_pos = 0
-        self._prefetch_next, self._prefetched, self._last_phase = None, False, None
         self._zeroed = set()   # groups whose grads the last fused step left zeroed
         self.noise = None
 
@@ -611,7 +610,6 @@ class SACEngine:
         self._run_bwd_multi('c.b' + str(int(dist)), lambda: [
             fill_bwd(heads, [None, ws['c.dmu'], ws['c.dls']][:len(heads)], B, trunk=True, upstream=UPSTREAM_CERT),
             fill_bwd([n['q0'], n['q1']], [ws['c.dq0'], ws['c.dq1']], B, upstream=UPSTREAM_CRITIC)], head=ch)
-        self._batch_done('critic')     # the batch buffers' last reader is enqueued
         tsy = n['cc_trunk'].sy
         items = [(n['q0'], [xs, n['q0'].sy[0], n['q0'].sy[1]], 'c'), (n['q1'], [xs, n['q1'].sy[0], n['q1'].sy[1]], 'c'),
                  (n['cc_trunk'], [xs, tsy[0]], 'cc'), (n['cc_mean'], [tsy[-1], n['cc_mean'].sy[0]], 'cc')]
@@ -705,7 +703,6 @@ class SACEngine:
             self._cc_bound_after('a.ccm', sqc, dist)
             self._run_fwd('a.mult', lambda: fill_fwd([self._out_net(n['mult'], 'a.multx', B)],
                                                      [(self.bs, S), (sqc, 1), (None, 0)], B))
-        self._batch_done('actor')
         # The actor losses' output gradients are formed inside the two backward launches
         # (drpo_actor_head_t): w.r.t. Q_k (-1/B) and the constraint critic's heads at (s, a)
         # (lam / B on the max-C bound; lam = MLPMultiplier's output transform of 'a.multx',
@@ -861,7 +858,6 @@ class SACEngine:
         self._cc_bound_after('m.ccs', sqc, dist)
         xm = self.buf('m.x', B, S + 1)
         self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B, save_x=xm))
-        self._batch_done('mult')
         gx = self.buf('m.gx', B)
         mc = sol.mlp_multiplier_cfg
         _lib.check(L.drpo_multiplier_head(B, n['mult'].sy[-1].data_ptr(), sqc.data_ptr(), aqc.data_ptr(),
@@ -907,7 +903,6 @@ class SACEngine:
             self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc,
                       dist)], ctr)
         self._cc_bound_after('m.cc', aqc, dist)
-        self._batch_done('mult')
         psum = self._loss_slots(1)
         _lib.check(L.drpo_multiplier_head(B, None, None, aqc.data_ptr(), float(sol.constraint_threshold),
                                           float(sol.penalty_lb), float(sol.penalty_ub), 0.0, 0.0, None,
@@ -918,37 +913,12 @@ class SACEngine:
                                 grad_from_sum_kind=1)])
 
     # ------------------------------------------------------------------
-    # ---- minibatch prefetch (production noise): the next update's drpo_sample_batch runs on
-    # a side stream once this update's last reader of the batch buffers is enqueued, so it
-    # overlaps this update's backward / weight-gradient / optimizer launches instead of
-    # opening the next update (5.9 us per update at B = 4096). The batch buffers are free
-    # by then: everything after the last forward reads the saves and the dZ buffers.
-    def _event(self):
-        ev = ctypes.c_void_p()
-        _lib.check(_lib.lib().drpo_event_create(ctypes.byref(ev)), 'event')
-        return ev
-
-    def _batch_done(self, phase):
-        """Called by each step after its last read of the batch buffers; fires the
-        prefetch at the update's last phase."""
-        pf = self._prefetch_next
-        if pf is None or phase != self._last_phase:
-            return
-        self._prefetch_next = None
-        L = _lib.lib()
-        if getattr(self, '_side', None) is None:
-            self._side = torch.cuda.Stream(device=self.dev)
-            self._ev_main, self._ev_side = self._event(), self._event()
-        side = ctypes.c_void_p(self._side.cuda_stream)
-        _lib.check(L.drpo_event_record(self._ev_main, _lib.stream()), 'event')
-        _lib.check(L.drpo_stream_wait_event(side, self._ev_main), 'stream wait')
-        self._sample_batch(*pf, stream=side)
-        _lib.check(L.drpo_event_record(self._ev_side, side), 'event')
-        self._prefetched = True
-
-    def _sample_batch(self, alg, noise, stream=None):
+    def update_solver(self, alg, update_actor, update_multiplier, noise):
+        """SMBPO.update_solver (src/smbpo.py:251-279) from the device-resident buffers."""
         sol = self.sol
         B = sol.batch_size
+        self._setup(B)
+        self.noise = noise
         n_real = int(alg.real_fraction * B)
         rb, vb = alg.replay_buffer._module, alg.virt_buffer._module
         ir = noise.randint(len(rb), n_real)
@@ -977,30 +947,10 @@ class SACEngine:
                                        float(alg.reward_scale), float(alg.alive_bonus), float(alg.constraint_scale),
                                        float(alg.constraint_offset), self.bs.data_ptr(), self.ba.data_ptr(),
                                        self.bs2.data_ptr(), self.br.data_ptr(), self.bd.data_ptr(),
-                                       self.bv.data_ptr(), self.bh.data_ptr(), stream or _lib.stream()),
-                   'sample_batch')
-
-    def update_solver(self, alg, update_actor, update_multiplier, noise, prefetch_next=False):
-        """SMBPO.update_solver (src/smbpo.py:251-279) from the device-resident buffers.
-        prefetch_next (production noise only): draw and gather the NEXT update's minibatch
-        on a side stream as soon as this update no longer reads the batch buffers."""
-        sol = self.sol
-        B = sol.batch_size
-        self._setup(B)
-        self.noise = noise
-        if getattr(self, '_prefetched', False):
-            # this update's minibatch was gathered by the previous update's prefetch
-            _lib.check(_lib.lib().drpo_stream_wait_event(_lib.stream(), self._ev_side), 'stream wait')
-            self._prefetched = False
-        else:
-            self._sample_batch(alg, noise)
-        parity = getattr(noise, 'parity', True)
-        self._prefetch_next = (alg, noise) if prefetch_next and not parity else None
-        self._last_phase = 'mult' if update_multiplier else ('actor' if update_actor else 'critic')
+                                       self.bv.data_ptr(), self.bh.data_ptr(), _lib.stream()), 'sample_batch')
         lq, lqc = self._critic_step(noise)
         if update_actor:
             self._actor_step(noise)
         if update_multiplier:
             self._mult_step(noise)
-        self._prefetch_next = None
         return lq, lqc

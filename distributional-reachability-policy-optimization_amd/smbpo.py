@@ -20,8 +20,6 @@ Constructor signature, Config fields, buffers and state_dict layout follow the
 reference; ``noise`` (DeviceNoise by default, TapeNoise for parity replays)
 supplies every random draw.
 """
-import os
-
 import numpy as np
 import torch
 
@@ -36,10 +34,6 @@ from .policy import UniformPolicy
 from .rng import DeviceNoise
 from .ssac import SSAC
 from .torch_util import Module, device as default_device, pythonic_mean
-
-# the next update's minibatch gathered on a side stream while the current update finishes
-# (production noise; SACEngine._batch_done). DRPO_PREFETCH_BATCHES=0: A/B.
-PREFETCH_BATCHES = os.environ.get('DRPO_PREFETCH_BATCHES', '1') != '0'
 
 N_EVAL_TRAJ = 10
 LOSS_AVERAGE_WINDOW = 10
@@ -274,23 +268,20 @@ class SMBPO(Configurable, Module):
         self.solver.update_r_bounds(r_min + self.alive_bonus, r_max + self.alive_bonus)
         return losses
 
-    def update_solver(self, update_actor=True, update_multiplier=False, noise=None, prefetch_next=False):
-        """src/smbpo.py:251-279: mixed real/virtual minibatch + critic/actor/multiplier updates.
-        prefetch_next: another update_solver call follows (rollout_and_update), so the next
-        minibatch may be gathered while this update finishes (production noise only)."""
+    def update_solver(self, update_actor=True, update_multiplier=False, noise=None):
+        """src/smbpo.py:251-279: mixed real/virtual minibatch + critic/actor/multiplier updates."""
         eng = self.solver.engine
         noise = self.noise if noise is None else noise
-        lq, lqc = eng.update_solver(self, update_actor, update_multiplier, noise, prefetch_next=prefetch_next)
+        lq, lqc = eng.update_solver(self, update_actor, update_multiplier, noise)
         self.recent_critic_losses.append(lq)
         self.recent_cons_critic_losses.append(lqc)
 
     def rollout_and_update(self, noise=None):
         self.rollout(self.actor, noise=noise)
-        n = self.solver_updates_per_step
-        for step in range(n):
+        for step in range(self.solver_updates_per_step):
             self.update_solver(update_actor=step % self.sac_cfg.actor_update_interval == 0,
                                update_multiplier=step % self.sac_cfg.multiplier_update_interval == 0,
-                               noise=noise, prefetch_next=step + 1 < n and PREFETCH_BATCHES)
+                               noise=noise)
 
     # ------------------------------------------------------------------ driver surface
     def setup(self):
