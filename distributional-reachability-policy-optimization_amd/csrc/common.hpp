@@ -555,14 +555,13 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
 // value that thread (< 256) needs for the finish.
 template <int ACT>
 __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const float* __restrict__ P,
-                                                const float* __restrict__ bias, float* out, int ldo, float* red,
-                                                const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+                                                const float* __restrict__ bias, float* out, int ldo, float* red) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
   if (wave < 4) {
     const int col = 192 + (threadIdx.x & 15);
-    const float b12 = (bias && col < 200) ? gload(bias + col) : 0.f;
-    tile_dense_core<8, 1, 2, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, gs);
+    const float b12 = col < 200 ? gload(bias + col) : 0.f;
+    tile_dense_core<8, 1, 2, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
     return b12;
   }
   const int q = wave - 4;
@@ -570,7 +569,7 @@ __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const 
   f32x4 bq[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) bq[u] = load_pk(P, 12, ks0 + (u < nks ? u : nks - 1), 13);
-  tile_dense_core<8, 1, 1, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, gs);
+  tile_dense_core<8, 1, 1, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -585,21 +584,13 @@ __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const 
   return 0.f;
 }
 
-// after a barrier: block 12 = the 4 partials (fixed order) + bias, activation, the
-// optional global saves (post- / pre-activation) of the tile's first gs.nrows rows
 template <int ACT>
-__device__ __forceinline__ void tile_dense_13s_finish(const float* red, float b12, float* out, int ldo,
-                                                      const GSave& gs = GSave{nullptr, nullptr, 0, 0}) {
+__device__ __forceinline__ void tile_dense_13s_finish(const float* red, float b12, float* out, int ldo) {
   const int tid = threadIdx.x;
   if (tid < 256) {
-    const int r = tid >> 4, c = tid & 15, col = 192 + c;
+    const int r = tid >> 4, c = tid & 15;
     const float z = ((red[tid] + red[256 + tid]) + (red[512 + tid] + red[768 + tid])) + b12;
-    const float y = act_fn<ACT>(z);
-    out[r * ldo + col] = col < 200 ? y : 0.f;
-    if (col < 200 && r < gs.nrows) {
-      if (gs.gy) gstore(gs.gy + (size_t)r * gs.ldg + col, y);
-      if (gs.gz) gstore(gs.gz + (size_t)r * gs.ldg + col, z);
-    }
+    out[r * ldo + 192 + c] = 192 + c < 200 ? act_fn<ACT>(z) : 0.f;
   }
 }
 

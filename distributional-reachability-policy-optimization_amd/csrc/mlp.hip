@@ -68,28 +68,18 @@ DRPO_API int drpo_debug_stamps(unsigned long long* dst, int n) {
   do {            \
   } while (0)
 #endif
-#ifndef DRPO_MLP_13S
-#define DRPO_MLP_13S 1   // A/B macro: 200x200 layers balanced over the SIMDs (tile_dense_13s)
-#endif
-
-template <int ACT, int RB, bool S13 = false>
+template <int ACT, int RB>
 __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const drpo_mlp_layer_t& L, const float* W,
                                               const float* b, float* out, int ldo, float* red, const GSave& gs) {
-  if (L.dout <= 16) {
+  if (L.dout <= 16)
     tile_dense_narrow<FW_NW, RB, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, red, gs);
-  } else if (S13 && DRPO_MLP_13S && RB == 1 && L.dout == 200 && L.din == 200) {
-    // 13 column blocks on 8 waves: the 13th split over K (3.25 blocks per SIMD, not 4)
-    const float b12 = tile_dense_13s<ACT>(in, ldi, W, b, out, ldo, red, gs);
-    lds_barrier();
-    tile_dense_13s_finish<ACT>(red, b12, out, ldo, gs);
-  } else {
+  else
     tile_dense<FW_NW, RB, FW_MAXC, ACT>(in, ldi, L.din, W, b, L.dout, out, ldo, gs);
-  }
 }
 
 // one layer of a (16*RB)-row tile: packed weights of batch item z, bias, activation,
 // optional global saves of the post-/pre-activation for the backward pass
-template <int RB = 1, bool S13 = false>
+template <int RB = 1>
 __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_mlp_layer_t& __restrict__ L, int z, int64_t rows,
                                           int row0, int nrows, float* out, float* red, bool save = true) {
   const float* W = L.W + (size_t)z * L.wstride;
@@ -97,10 +87,10 @@ __device__ __forceinline__ void run_layer(const float* in, int ldi, const drpo_m
   const size_t so = ((size_t)z * rows + row0) * L.dout;
   GSave gs{save && L.sy ? L.sy + so : nullptr, save && L.sz ? L.sz + so : nullptr, L.dout, nrows};
   switch (L.act) {
-    case ACT_RELU: run_layer_act<ACT_RELU, RB, S13>(in, LDH, L, W, b, out, LDH, red, gs); break;
-    case ACT_SILU: run_layer_act<ACT_SILU, RB, S13>(in, LDH, L, W, b, out, LDH, red, gs); break;
-    case ACT_TANH: run_layer_act<ACT_TANH, RB, S13>(in, LDH, L, W, b, out, LDH, red, gs); break;
-    default: run_layer_act<ACT_NONE, RB, S13>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_RELU: run_layer_act<ACT_RELU, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_SILU: run_layer_act<ACT_SILU, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    case ACT_TANH: run_layer_act<ACT_TANH, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
+    default: run_layer_act<ACT_NONE, RB>(in, LDH, L, W, b, out, LDH, red, gs); break;
   }
   (void)ldi;
 }
@@ -116,7 +106,7 @@ __device__ __forceinline__ float* run_net(const drpo_mlp_fwd_t& a, float* in, fl
   for (int l = 0; l < MAXL; ++l) {
     if (l < a.net[NI].nl) {
       float* out = (cur == bufA) ? bufB : bufA;
-      run_layer<1, true>(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red, save);
+      run_layer(cur, LDH, a.net[NI].L[l], z, a.rows, row0, nrows, out, red, save);
       lds_barrier();
       STAMP(2 + 4 * NI + l);
       cur = out;
@@ -503,7 +493,7 @@ __device__ __forceinline__ float act_grad_saved(int act, float saved) {
 
 // G (LDS, width of the net output) -> gradient w.r.t. the net input (returned LDS buffer)
 __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__ net, float* G, float* bA, float* bB, int z, int64_t rows,
-                          int row0, int nrows, bool need_dx0, bool alt = false, float* red = nullptr) {
+                          int row0, int nrows, bool need_dx0, bool alt = false) {
   const int tid = threadIdx.x;
   float* cur = G;
   float sv[BW_PER];
@@ -534,13 +524,7 @@ __device__ __forceinline__ float* bwd_net(const drpo_mlp_bwd_net_t& __restrict__
     if (l > 0) bwd_fetch_act(net.L[l - 1], z, rows, row0, nrows, sv);   // next layer's, during this GEMM
     float* out = (cur == bA) ? bB : bA;
     // dY_prev = dZ W: transposed mirror, N = din, K = dout
-    if (DRPO_MLP_13S && red && din == 200 && dout == 200) {   // SIMD-balanced 200x200 (scratch: red)
-      tile_dense_13s<ACT_NONE>(cur, LDH, W, nullptr, out, LDH, red);
-      lds_barrier();
-      tile_dense_13s_finish<ACT_NONE>(red, 0.f, out, LDH);
-    } else {
-      tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, dout, W, nullptr, din, out, LDH);
-    }
+    tile_dense<FW_NW, 1, FW_MAXC, ACT_NONE>(cur, LDH, dout, W, nullptr, din, out, LDH);
     lds_barrier();
     cur = out;
   }
@@ -985,15 +969,15 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
     }
     if (!up) load_gout(n, G);
     STAMPW(1);
-    float* gh = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, true, false, DT);
+    float* gh = bwd_net(n, G, bA, bB, z, a.rows, row0, nrows, true);
     STAMPW(2);
-    bwd_net(a.net[0], gh, bA, bB, z, a.rows, row0, nrows, false, sel == 1, DT);
+    bwd_net(a.net[0], gh, bA, bB, z, a.rows, row0, nrows, false, sel == 1);
     STAMPW(12);
     return;
   }
   if (bwd_paired_heads(a)) {
     bwd_heads_paired<UPF>(a, G, bA, bB, DT, z, row0, nrows, hc, a.upstream == DRPO_UPSTREAM_ENS ? eu : nullptr, ha);
-    const float* gx = bwd_net(a.net[0], G, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr, false, DT);
+    const float* gx = bwd_net(a.net[0], G, bA, bB, z, a.rows, row0, nrows, a.net[0].dx != nullptr);
     STAMPW(12);
     if (gx) store_dx(a.net[0], gx);
     return;
