@@ -150,3 +150,37 @@ def test_wgrad_rejects_shared_gradient_and_small_workspace():
     it.dout, it.din, it.rows, it.nbatch = 256, 256, 4096, 1
     it.zstride, it.ystride, it.gwstride, it.gbstride = 4096 * 256, 4096 * 256, 65536, 256
     assert L.drpo_mlp_wgrad(arr1, 1, ws.data_ptr(), 16, _lib.stream()) != 0
+
+
+@pytest.mark.parametrize('rows', [37, 1792, 4096])
+def test_wgrad_second_dz_term(rows):
+    """drpo_wgrad_item_t.dz2 (the split-heads fit backward's trunk dZ = dz + dz2): the
+    product is (dz + dz2)^T y and the bias colsum(dz + dz2), for 64-, 16- and odd-width
+    tiles, ensemble batches and several row chunks."""
+    L = _lib.lib()
+    nb = 3
+    shapes = [(200, 200), (200, 14), (13, 200)]
+    items = make_items(shapes, rows, nbatch=nb, seed=rows + 7)
+    g = torch.Generator().manual_seed(rows)
+    arr = (WgradItem * len(items))()
+    for k, d in enumerate(items):
+        d['dz2'] = torch.randn(nb, rows, d['dout'], generator=g).to(DEV)
+        it = arr[k]
+        it.dz, it.y, it.gW, it.gb = d['dz'].data_ptr(), d['y'].data_ptr(), d['gW'].data_ptr(), d['gb'].data_ptr()
+        it.dz2 = d['dz2'].data_ptr()
+        it.dout, it.din, it.rows, it.nbatch = d['dout'], d['din'], rows, nb
+        it.zstride, it.ystride, it.gwstride, it.gbstride = rows * d['dout'], rows * d['din'], d['dout'] * d['din'], \
+            d['dout']
+    need = L.drpo_mlp_wgrad_workspace_size(arr, len(items))
+    ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=DEV)
+    _lib.check(L.drpo_mlp_wgrad(arr, len(items), ws.data_ptr(), ws.numel(), _lib.stream()), 'wgrad')
+    torch.cuda.synchronize()
+    for d in items:
+        dz = (d['dz'] + d['dz2']).double().cpu()
+        y = d['y'].double().cpu()
+        gW = torch.einsum('zro,zri->zoi', dz, y)
+        gb = dz.sum(1)
+        scale = 1e-5 * np.sqrt(rows) * max(float(gW.abs().max()), 1.0)
+        for got, ref, what in ((d['gW'], gW, 'gW'), (d['gb'], gb, 'gb')):
+            err = (got.double().cpu() - ref).abs()
+            assert bool((err <= scale + 1e-5 * ref.abs()).all()), f'{what} {d["dout"]}x{d["din"]}: {float(err.max())}'
