@@ -7,17 +7,39 @@
 
 namespace drpo {
 
-__device__ __forceinline__ float sp_grad(float x) { return x > 20.f ? 1.f : 1.f / (1.f + expf(-x)); }
+// Transcendentals of the per-row critic math. The libm forms (range reduction, IEEE
+// division) made the certificate upstream of the critic backward a 15.5 k-cycle serial
+// chain per workgroup (profiles/sac_stamps.py); the hardware forms (v_exp_f32 /
+// v_log_f32 / v_rcp_f32, ~1 ulp) cut it, at ~1e-6 relative error -- far inside the SAC
+// parity tolerances. log1p of a small argument uses its series (log(1 + y) alone loses
+// the low bits of y). DRPO_CRITIC_FAST_MATH=0: the libm forms (A/B).
+#ifndef DRPO_CRITIC_FAST_MATH
+#define DRPO_CRITIC_FAST_MATH 1
+#endif
+__device__ __forceinline__ float cr_exp(float x) { return DRPO_CRITIC_FAST_MATH ? fast_exp(x) : expf(x); }
+__device__ __forceinline__ float cr_log(float x) {
+  return DRPO_CRITIC_FAST_MATH ? 0.69314718055994531f * __builtin_amdgcn_logf(x) : logf(x);
+}
+__device__ __forceinline__ float cr_rcp(float x) { return DRPO_CRITIC_FAST_MATH ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
+__device__ __forceinline__ float cr_softplus(float x) {   // torch softplus (beta 1, threshold 20)
+  if (!DRPO_CRITIC_FAST_MATH) return softplusf(x);
+  if (x > 20.f) return x;
+  const float y = fast_exp(-fabsf(x));
+  const float l1p = y < 1e-3f ? y * (1.f - 0.5f * y) : 0.69314718055994531f * __builtin_amdgcn_logf(1.f + y);
+  return fmaxf(x, 0.f) + l1p;
+}
+
+__device__ __forceinline__ float sp_grad(float x) { return x > 20.f ? 1.f : cr_rcp(1.f + cr_exp(-x)); }
 
 __device__ __forceinline__ float cc_std(float l, float lmin, float lmax) {
-  float ls = lmax - softplusf(lmax - l);
-  ls = lmin + softplusf(ls - lmin);
-  return expf(ls);
+  float ls = lmax - cr_softplus(lmax - l);
+  ls = lmin + cr_softplus(ls - lmin);
+  return cr_exp(ls);
 }
 
 // d std / d raw for std = exp(lmin + sp(lmax - sp(lmax - l) - lmin))
 __device__ __forceinline__ float cc_dstd_draw(float l, float lmin, float lmax, float std) {
-  const float ls1 = lmax - softplusf(lmax - l);
+  const float ls1 = lmax - cr_softplus(lmax - l);
   return std * sp_grad(ls1 - lmin) * sp_grad(lmax - l);
 }
 
@@ -59,12 +81,13 @@ __device__ __forceinline__ float cert_element(const Head& p, int64_t i, int c, f
     const float yb = diff + mu;
     const float sd = cc_std(p.ls[k], p.lmin, p.lmax);
     const float var = sd * sd;
-    const float t1 = (mu - yc) * (mu - yc) / (2.f * var);
-    const float t2 = (mu - yb) * (mu - yb) / (2.f * var);
-    dmu = (mu - yc) / var * invN;
-    const float dsd = (-(mu - yb) * (mu - yb) / (var * sd) + 1.f / sd) * invN;
+    const float ivar = cr_rcp(var), isd = cr_rcp(sd);
+    const float t1 = (mu - yc) * (mu - yc) * (0.5f * ivar);
+    const float t2 = (mu - yb) * (mu - yb) * (0.5f * ivar);
+    dmu = (mu - yc) * ivar * invN;
+    const float dsd = (-(mu - yb) * (mu - yb) * ivar * isd + isd) * invN;
     dls = dsd * cc_dstd_draw(p.ls[k], p.lmin, p.lmax, sd);
-    return (t1 + t2 + logf(sd)) * invN;
+    return (t1 + t2 + cr_log(sd)) * invN;
   }
   dmu = 2.f * (mu - yc) * invN;
   dls = 0.f;
