@@ -173,7 +173,8 @@ __device__ __forceinline__ float normal_at(const float* eps, int64_t idx, uint64
   if (eps) return eps[idx];
   float z[4];
   philox_normal4(seed, (uint32_t)(idx >> 2), (uint32_t)(idx >> 34), site, (uint32_t)ctr, z);
-  return z[idx & 3];
+  const int j = (int)(idx & 3);   // selects, not an indexed (private-memory) array
+  return j == 0 ? z[0] : (j == 1 ? z[1] : (j == 2 ? z[2] : z[3]));
 }
 
 // squashed-Gaussian head of one row (src/policy.py:88-97; Independent(Tanh(Normal))

@@ -48,10 +48,12 @@ __device__ __forceinline__ float cc_dstd_draw(float l, float lmin, float lmax, f
 // soft Bellman target of row i with the twin-min target critics (src/ssac.py:284-294)
 template <typename Head>
 __device__ __forceinline__ float critic_target(const Head& p, int64_t i, float alpha) {
-  float nv = fminf(p.q0t[i], p.q1t[i]);
-  if (!p.deterministic_backup) nv = nv - alpha * p.logp2[i];
-  const float dn = p.d[i] ? 1.f : 0.f;
-  return p.r[i] + p.discount * (1.f - dn) * nv;
+  // global-address-space loads (gload): the descriptor's pointers are generic, and FLAT
+  // loads would also count against lgkmcnt and drain with every LDS wait
+  float nv = fminf(gload(p.q0t + i), gload(p.q1t + i));
+  if (!p.deterministic_backup) nv = nv - alpha * gload(p.logp2 + i);
+  const float dn = gload(p.d + i) ? 1.f : 0.f;
+  return gload(p.r + i) + p.discount * (1.f - dn) * nv;
 }
 
 // certificate element k = (i, c): reachability backup (src/ssac.py:304-413), the
@@ -61,32 +63,35 @@ template <typename Head>
 __device__ __forceinline__ float cert_element(const Head& p, int64_t i, int c, float& dmu, float& dls) {
   const int64_t k = i * p.C + c;
   const float invN = 1.f / (float)(p.B * p.C);
-  const float dn = p.d[i] ? 1.f : 0.f;
+  const float dn = gload(p.d + i) ? 1.f : 0.f;
   // certificate-target done flags: the batch's, or the model-predicted ones of the
   // robust branch (src/ssac.py:387-400)
-  const float dnc = p.dc ? (p.dc[i] ? 1.f : 0.f) : dn;
-  const float hv = p.h[k];
-  const float mu = p.mu[k];
+  const float dnc = p.dc ? (gload(p.dc + i) ? 1.f : 0.f) : dn;
+  const float hv = gload(p.h + k);
+  const float mu = gload(p.mu + k);
+  const float mut = gload(p.mu_t + k);
+  const float lst = p.distributional ? gload(p.ls_t + k) : 0.f;
+  const float lsk = p.distributional ? gload(p.ls + k) : 0.f;
   float q2;
   if (p.distributional) {
     const float e = fminf(fmaxf(normal_at(p.eps3, k, p.seed, p.ctr, 7u), -2.f), 2.f);
-    q2 = p.mu_t[k] + e * cc_std(p.ls_t[k], p.lmin, p.lmax);
+    q2 = mut + e * cc_std(lst, p.lmin, p.lmax);
   } else {
-    q2 = p.mu_t[k];
+    q2 = mut;
   }
   const float nonterm = (1.f - p.discount) * hv + p.discount * fmaxf(hv, q2);
   const float yc = nonterm * (1.f - dnc) + hv * dnc;
   if (p.distributional) {
     const float diff = fminf(fmaxf(yc - mu, -p.qc_td_bound), p.qc_td_bound);
     const float yb = diff + mu;
-    const float sd = cc_std(p.ls[k], p.lmin, p.lmax);
+    const float sd = cc_std(lsk, p.lmin, p.lmax);
     const float var = sd * sd;
     const float ivar = cr_rcp(var), isd = cr_rcp(sd);
     const float t1 = (mu - yc) * (mu - yc) * (0.5f * ivar);
     const float t2 = (mu - yb) * (mu - yb) * (0.5f * ivar);
     dmu = (mu - yc) * ivar * invN;
     const float dsd = (-(mu - yb) * (mu - yb) * ivar * isd + isd) * invN;
-    dls = dsd * cc_dstd_draw(p.ls[k], p.lmin, p.lmax, sd);
+    dls = dsd * cc_dstd_draw(lsk, p.lmin, p.lmax, sd);
     return (t1 + t2 + cr_log(sd)) * invN;
   }
   dmu = 2.f * (mu - yc) * invN;
