@@ -640,12 +640,12 @@ __device__ __forceinline__ void ens_upstream(EnsUpK& u, const drpo_mlp_bwd_net_t
     if (r < nrows && k < S1) {
       const int64_t row = row0 + r;
       const int64_t o = ((int64_t)z * b + row) * S1 + k;
-      const float hi = u.maxlv[k], lo = u.minlv[k];
-      const float raw = u.LVR[o];
+      const float hi = gload(u.maxlv + k), lo = gload(u.minlv + k);
+      const float raw = gload(u.LVR + o);
       const float l1 = hi - softplusf(hi - raw);
       const float l = lo + softplusf(l1 - lo);
-      const float m = u.D[o] + (k < S ? u.s[(int64_t)z * u.s_zstride + row * S + k] : 0.f);
-      const float diff = u.t[(int64_t)z * u.t_zstride + row * S1 + k] - m;
+      const float m = gload(u.D + o) + (k < S ? gload(u.s + (int64_t)z * u.s_zstride + row * S + k) : 0.f);
+      const float diff = gload(u.t + (int64_t)z * u.t_zstride + row * S1 + k) - m;
       const float iv = expf(-l);
       acc += diff * diff * iv + l;
       const float dl = (1.f - diff * diff * iv) * g;
@@ -717,14 +717,14 @@ __device__ __forceinline__ void actor_cc_upstream(ActorHeadK& h, int side, const
       float best = 0.f, lbest = 0.f;
       int bi = 0;
       for (int c = 0; c < C; ++c) {
-        float v = mu[i * C + c];
-        const float l = dist ? ls[i * C + c] : 0.f;
+        float v = gload(mu + i * C + c);
+        const float l = dist ? gload(ls + i * C + c) : 0.f;
         if (dist) v = v + h.std_ratio * cc_std(l, h.log_std_min, h.log_std_max);
         if (c == 0 || v > best) { best = v; bi = c; lbest = l; }
       }
       float g = invB;
       if (side == 0) {
-        float lam = h.lams ? h.lams[i] : h.fixed_lam;
+        float lam = h.lams ? gload(h.lams + i) : h.fixed_lam;
         const float ub = h.lam_upper_bound;
         if (h.lams && ub > 0.f) lam = ub / 2.f * (1.f + tanhf(lam / ub * 2.f));   // MLPMultiplier.forward
         if (!h.lams && (best < h.clamp_lb || best > h.clamp_ub)) lam = 0.f;       // clamped scalar-lam term
@@ -766,9 +766,9 @@ __device__ __forceinline__ void squash_upstream(ActorHeadK& h, int side, const d
     if (r < nrows && k < 2 * A) {
       const int64_t i = row0 + r;
       const int d = k < A ? k : k - A;
-      const float mu = raw[i * 2 * A + d], rr = raw[i * 2 * A + A + d];
-      const float uu = u[i * A + d], ee = ep[i * A + d];
-      const float dAv = dA2 ? dA[i * A + d] + dA2[i * A + d] : dA[i * A + d];
+      const float mu = gload(raw + i * 2 * A + d), rr = gload(raw + i * 2 * A + A + d);
+      const float uu = gload(u + i * A + d), ee = gload(ep + i * A + d);
+      const float dAv = dA2 ? gload(dA + i * A + d) + gload(dA2 + i * A + d) : gload(dA + i * A + d);
       const float sg = sigmoidf(rr);
       const float sd = expf(-6.f + 10.f * sg) * 1.0f;
       const float a = tanhf(uu);
@@ -781,7 +781,7 @@ __device__ __forceinline__ void squash_upstream(ActorHeadK& h, int side, const d
         const float dsd = du * ee + glp * (diff * diff / (var * sd) - 1.f / sd);
         gv = dsd * sd * 10.f * sg * (1.f - sg);
       }
-      if (side == 0 && h.alpha_sum && k == 0) asum = h.logp[i] + h.target_entropy;
+      if (side == 0 && h.alpha_sum && k == 0) asum = gload(h.logp + i) + h.target_entropy;
     }
     G[r * LDH + k] = gv;
   }
@@ -927,7 +927,7 @@ __device__ __forceinline__ void bwd_body(const drpo_mlp_bwd_t& __restrict__ a, i
           const int64_t i = row0 + r;
           const float invB = 1.f / (float)hq->B;
           const float y = critic_target(*hq, i, expf(*hq->log_alpha));
-          const float err = (sel ? hq->q1[i] : hq->q0[i]) - y;
+          const float err = gload((sel ? hq->q1 : hq->q0) + i) - y;
           g = err * invB;
           lq = err * err * (0.5f * invB);
         }

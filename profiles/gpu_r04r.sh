@@ -1,4 +1,4 @@
-OUT=gpurun_out/r04r
+OUT=gpurun_out/${1:-r04r}
 mkdir -p $OUT
 export TMPDIR=/tmp
 LIBD=$PWD/distributional-reachability-policy-optimization_amd
