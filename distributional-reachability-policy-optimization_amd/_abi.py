@@ -214,6 +214,7 @@ PROTOTYPES.update({
     'drpo_mlp_wgrad_reduce': (c_int, [POINTER(WgradItem), c_int, POINTER(EnsReduce), P, c_size_t, P]),
     'drpo_mlp_wgrad_sums': (c_int, [POINTER(WgradItem), c_int, POINTER(SumDesc), c_int, P, c_size_t, P]),
     'drpo_mlp_wgrad_adam': (c_int, [POINTER(WgradItem), c_int, P, POINTER(WgradAdam), P, c_size_t, P]),
+    'drpo_ens_loss_reduce': (c_int, [POINTER(EnsReduce), P]),
     'drpo_sample_batch': (c_int, [POINTER(BufferView), POINTER(BufferView), c_int, c_int, c_int, c_int, c_int, P, P,
                                   c_uint64, c_uint64, c_float, c_float, c_float, c_float, P, P, P, P, P, P, P, P]),
     'drpo_policy_head': (c_int, [P, c_int64, c_int, c_int, P, c_uint64, c_uint64, ctypes.c_uint32, P, P, P, P, P,

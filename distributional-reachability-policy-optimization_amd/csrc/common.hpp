@@ -315,6 +315,28 @@ __device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N,
   }
 }
 
+// LDS stores of MFMA accumulators. A 16x16 accumulator's register r holds row 4g + r
+// (g = lane >> 4) of column lane & 15, and ds_write_b32 banks a wave's 64 lanes in two
+// 32-lane groups by dword address mod 32 (MI355X_MICROARCH.md, LDS). With a row stride
+// == 8 (mod 32) (lds_ld: the A-fragment reads' conflict-free stride) lane groups g = 2h
+// and 2h + 1 of one store land on the SAME 16 banks (rows 4 apart: 32 dwords): a 2-way
+// conflict on every epilogue store -- the 24.9 % "bank conflict" cycles of the SAC
+// forward's PMC (profiles/r04/pmc_sac). A 2-way conflict on ds_write_b32 fits inside the
+// store's own 4-cycle transfer, so it costs no time; the conflict-free order below (lanes
+// of odd g store register r ^ 2, row 4g + (r ^ 2): 16 banks away; r ^ 1 for the
+// 16-float-stride partial slabs) costs a lane select per store and measured SLOWER on
+// one box, alternating (profiles/r05/swz_ab: rollout frac 0.434-0.435 vs 0.466, SAC 63.5
+// vs 65.7 TFLOP/s, fit 0.0757 vs 0.0735 ms). Kept as an A/B macro, off.
+#ifndef DRPO_LDS_SWZ
+#define DRPO_LDS_SWZ 0   // A/B macro, measured slower (profiles/r05/swz_ab): off
+#endif
+template <int X>
+__device__ __forceinline__ int swz_row(int r, int g) { return DRPO_LDS_SWZ ? r ^ (X * (g & 1)) : r; }
+template <int X>
+__device__ __forceinline__ float swz_pick(const f32x4& v, int r, int g) {
+  return (DRPO_LDS_SWZ && (g & 1)) ? v[r ^ X] : v[r];
+}
+
 template <int NW, int RB, int MAXC, int ACT>
 __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], const float (&bvs)[MAXC], int N,
                                                float* out, int ldo, const GSave& gs) {
@@ -331,8 +353,8 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + r;
-        const float z = acc[rb][c][r] + bv;
+        const int row = rb * 16 + 4 * g + swz_row<2>(r, g);
+        const float z = swz_pick<2>(acc[rb][c], r, g) + bv;
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
         if (col < N && row < gs.nrows) {
@@ -581,7 +603,7 @@ __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const 
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[q * 256 + (4 * g + r) * 16 + l15] = acc[r];
+  for (int r = 0; r < 4; ++r) red[q * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc, r, g);
   return 0.f;
 }
 
@@ -672,7 +694,7 @@ __device__ __forceinline__ void tile_dense_narrow_partials(const float* in, int 
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
   lds_barrier();
 }
 
@@ -723,7 +745,7 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
   lds_barrier();
   for (int e = tid; e < RB * 256; e += NW * 64) {
     const int rb = e >> 8, rr = (e >> 4) & 15, col = e & 15;
@@ -822,8 +844,8 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + r;
-        const float z = acc[rb][c][r] + bvs[c];
+        const int row = rb * 16 + 4 * g + swz_row<2>(r, g);
+        const float z = swz_pick<2>(acc[rb][c], r, g) + bvs[c];
         const float y = act_fn<ACT>(z);
         out[row * ldo + col] = (col < nn) ? y : 0.f;
         if (col < nn && row < gs.nrows) {
@@ -942,8 +964,8 @@ __device__ __forceinline__ void tile_dense_pair2_core(const float* in1, const fl
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + r;
-        const float z = acc[rb][c][r] + bvs[c];
+        const int row = rb * 16 + 4 * g + swz_row<2>(r, g);
+        const float z = swz_pick<2>(acc[rb][c], r, g) + bvs[c];
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < nn) ? y : 0.f;
         if (col < nn && row < gs.nrows) {
@@ -1111,7 +1133,7 @@ __device__ __forceinline__ void tile_dense_narrow_pair_partials(const float* in1
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
   lds_barrier();
 }
 
@@ -1161,7 +1183,7 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
   lds_barrier();
   for (int e = tid; e < 2 * RB * 256; e += NW * 64) {
     const int which = e / (RB * 256), e2 = e - which * RB * 256;

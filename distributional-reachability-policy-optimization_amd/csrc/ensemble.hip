@@ -309,3 +309,12 @@ DRPO_API int drpo_ens_loss_partials(const float* D, const float* LVR, const floa
   return ens_loss_launch(D, LVR, s, s_zstride, t, t_zstride, b, S, Z, minlv, maxlv, weight, gscale, mse, loss, gD,
                          gLVR, gmin, gmax, workspace, reduce_out, stream);
 }
+
+DRPO_API int drpo_ens_loss_reduce(const drpo_ens_reduce_t* red, drpo_stream_t stream) {
+  DRPO_REQUIRE(red && red->part && red->mse && red->Z >= 1 && red->Z <= 256 && red->S1 >= 1 &&
+                   red->S1 <= LOSS_MAXS1 && red->nbx >= 1 && red->minlv && red->maxlv,
+               "drpo_ens_loss_reduce: bad reduction");
+  ens_loss_reduce_kernel<<<1, 256, 0, (hipStream_t)stream>>>(*red);
+  DRPO_LAUNCH_CHECK("ens_loss_reduce");
+  return DRPO_OK;
+}

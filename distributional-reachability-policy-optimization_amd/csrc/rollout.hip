@@ -589,8 +589,8 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float y = act_fn<ACT_SILU>(acc[rb][c][r] + bvs[c]);
-        out[(rb * 16 + 4 * g + r) * ldo + col] = col < N ? y : 0.f;
+        const float y = act_fn<ACT_SILU>(swz_pick<2>(acc[rb][c], r, g) + bvs[c]);
+        out[(rb * 16 + 4 * g + swz_row<2>(r, g)) * ldo + col] = col < N ? y : 0.f;
       }
   }
   wave_lds_sync();
@@ -608,7 +608,7 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red_slot[rb * 256 + (4 * g + r) * 16 + l15] = pacc[rb][r];
+    for (int r = 0; r < 4; ++r) red_slot[rb * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(pacc[rb], r, g);
 }
 
 template <int NW, int RB, int NC, int NK>

@@ -27,6 +27,22 @@
 // That is MI355X_MICROARCH.md's validated hand-off (sc1 payload, drained, one
 // ticket add per workgroup, last arriver by the returned value, sc1 loads); nothing
 // ever waits, so no schedule can hang it.
+//
+// Memory-model note. Every operation of the hand-off is RELAXED (agent scope): the
+// slab stores, the ticket add and the slab loads. Under the C++ / HIP memory model
+// nothing orders the slab stores before the ticket or the ticket before the loads;
+// the hand-off is correct because of gfx950's ordering, not because of
+// release/acquire semantics:
+//   - an agent-scope relaxed store is a write-through `global_store ... sc1` (the bytes
+//     leave the XCD's L2 for the agent-coherent memory side);
+//   - `s_waitcnt vmcnt(0)` after the stores, then a workgroup barrier, then the one
+//     ticket add: the add issues only after every wave's stores have completed;
+//   - the last arriver learns it from the add's returned value and reads the slabs with
+//     `global_load ... sc1` (bypassing the per-CU L1, which is never refreshed by
+//     other CUs' stores), issued only after the add returned.
+// The __ATOMIC_ACQ_REL form of the ticket (DRPO_WGRAD_ACQREL=1, an A/B build) lowers to
+// `buffer_wbl2 sc1` + `buffer_inv sc1` around the add: a write-back of the XCD's whole L2
+// and an L1 invalidate, each ~1.7 us per workgroup (MI355X_MICROARCH.md, price list).
 #include "common.hpp"
 #include "ens_reduce.hpp"
 
@@ -39,6 +55,9 @@ constexpr int WG_NT = WG_NW * 64;
 #define DRPO_WG_D 3
 #endif
 constexpr int WG_D = DRPO_WG_D;          // register ring slots (k-groups of 4 rows each; A/B macro)
+#ifndef DRPO_WGRAD_ACQREL
+#define DRPO_WGRAD_ACQREL 0              // A/B macro: acq_rel ticket (see the memory-model note)
+#endif
 constexpr int WG_ROWQ = 64;              // chunk granularity (rows)
 constexpr int WG_MAXITEMS = 16;
 constexpr int WG_SLD = 264;              // LDS slab stride per accumulator block (== 8 mod 32)
@@ -76,6 +95,7 @@ struct WgradPlan {
   int va, vb;              // 16-byte loads of dZ / Y rows (widths % 4 == 0, aligned)
   int z2;                  // a second dZ term (item dz2)
   int pk_layer;            // fused Adam: the item's matrix in the pack map (-1: none)
+  int pk_z0;               // its first member within that matrix (a member shard's slice)
   int64_t first_unit;      // first logical workgroup of the item
   int64_t first_tile;      // first arrival counter of the item
   int64_t slab_off;        // first slab float of the item (tiles with nch > 1)
@@ -370,7 +390,9 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
     int& s_last = *reinterpret_cast<int*>(red + 4);
     if (tid == 0) {
       unsigned* c = a.ctr + P.first_tile + tile_local;
-      const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // relaxed: see the memory-model note at the top (gfx950 ordering, not C++ acq_rel)
+      const unsigned old = __hip_atomic_fetch_add(c, 1u, DRPO_WGRAD_ACQREL ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == (unsigned)(P.nch - 1);
       if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = last;
@@ -414,7 +436,7 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
     // gradient itself is never written (nonzero input terms are cleared)
     const drpo_pack_map_t* md = P.pk_layer >= 0 ? (const drpo_pack_map_t*)a.adam.map : nullptr;
     const int ncb = (dout + 15) >> 4, nks = (din + 15) >> 4;
-    const int64_t mb = md ? md->poff[P.pk_layer] + (int64_t)zb * ncb * nks * 256 : 0;
+    const int64_t mb = md ? md->poff[P.pk_layer] + (int64_t)(P.pk_z0 + zb) * ncb * nks * 256 : 0;
     float* PM = md ? md->P : nullptr;
     float* PTM = md ? md->PT : nullptr;
 #pragma unroll
@@ -708,11 +730,19 @@ static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_re
     for (int k = 0; k < p.a.n; ++k) {
       const drpo_wgrad_item_t& I = p.a.it[k];
       p.a.pl[k].pk_layer = -1;
+      p.a.pl[k].pk_z0 = 0;
       if (!mh) continue;
       const int64_t off = I.gW - adam->g;
-      for (int l = 0; l < mh->nlayers && l < 16; ++l)
-        if (mh->off[l] == off && mh->din[l] == I.din && mh->dout[l] == I.dout && mh->nbatch[l] == I.nbatch)
-          p.a.pl[k].pk_layer = l;
+      // the item is members [z0, z0 + nbatch) of one [nbatch][dout][din] matrix of the map
+      // (the whole matrix, or a member shard's contiguous slice of it)
+      for (int l = 0; l < mh->nlayers && l < 16; ++l) {
+        const int64_t per = (int64_t)mh->din[l] * mh->dout[l], rel = off - mh->off[l];
+        if (mh->din[l] != I.din || mh->dout[l] != I.dout || rel < 0 || rel % per != 0) continue;
+        const int64_t z0 = rel / per;
+        if (z0 + I.nbatch > mh->nbatch[l] || (I.nbatch > 1 && I.gwstride != per)) continue;
+        p.a.pl[k].pk_layer = l;
+        p.a.pl[k].pk_z0 = (int)z0;
+      }
       DRPO_REQUIRE(p.a.pl[k].pk_layer >= 0, "drpo_mlp_wgrad_adam: item %d is not a matrix of the pack map", k);
     }
   }

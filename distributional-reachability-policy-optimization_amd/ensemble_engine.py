@@ -48,6 +48,21 @@ def split_heads(n, Z):
     return (n + 15) // 16 * Z <= SPLIT_HEADS_MAX_TILES
 
 
+def ens_fused_shapes(nets, S1):
+    """The shapes drpo_mlp_backward_ens accepts (csrc/mlp.hip): both heads
+    [H -> 200|256 -> S+1] with the same hidden width and activation and an identity
+    output layer, S+1 <= 64, and every trunk layer at most 256 wide."""
+    h1, h2 = nets[1].layers, nets[2].layers
+    if len(h1) != 2 or len(h2) != 2 or S1 > 64:
+        return False
+    (_, _, _, hid1, act1, _), (_, _, _, hid2, act2, _) = h1[0], h2[0]
+    if hid1 not in (200, 256) or hid1 != hid2 or act1 != act2:
+        return False
+    if h1[1][3] != S1 or h2[1][3] != S1 or h1[1][4] != 0 or h2[1][4] != 0:
+        return False
+    return all(din <= 256 and dout <= 256 for (_, _, din, dout, _, _) in nets[0].layers)
+
+
 def split_heads_bwd(n, Z):
     if os.environ.get('DRPO_SPLIT_BWD', '1') == '0':     # A/B knob: the paired backward
         return False
@@ -379,9 +394,9 @@ class EnsembleEngine:
         bd, wl = self._backward_descs(nets, strides, save_x, gD, gL, b, Z)
         # the NLL loss rides in the backward launch (its output gradients formed in-kernel)
         # and its reduction in the weight-gradient launch: forward, backward, wgrad, Adam.
-        # That needs the paired-heads backward (200- or 256-wide heads, the reference
-        # default); other widths keep the separate loss launch.
-        fused = m.hidden_dim in (200, 256) and S1 <= 64
+        # That needs the shapes drpo_mlp_backward_ens takes (the reference default:
+        # head_hidden_layers=1, 200-wide); other shapes keep the separate loss launch.
+        fused = ens_fused_shapes(nets, S1)
         bd.upstream = 3 if fused else 0   # DRPO_UPSTREAM_ENS
         up = EnsUpstream()
         up.D, up.LVR = nets[1].sy[-1].data_ptr(), nets[2].sy[-1].data_ptr()

@@ -63,6 +63,11 @@ class EventTimer:
         return out
 
 
+_VB_FIELDS = ('_states', '_actions', '_next_states', '_rewards', '_constraint_values', '_dones', '_violations',
+              '_pointer')
+_ROLLOUT_CACHE_MAX = 8
+
+
 def _rollout_static(alg, policy, B, H):
     """The per-(shapes, parameter groups, buffers) part of the rollout descriptor: the
     packed-mirror and bias pointers, env parameters, normalizer / log-var bound and
@@ -73,12 +78,17 @@ def _rollout_static(alg, policy, B, H):
     vb = alg.virt_buffer._module
     pg, mg = policy.group, model.group
     norm = model.state_normalizer
+    # every device pointer the descriptor stores is part of the key (a buffer reallocated
+    # under one of them must never leave a stale pointer behind)
     key = (id(policy), B, H, pg.data.data_ptr(), pg.packed.data_ptr(), mg.data.data_ptr(), mg.packed.data_ptr(),
-           norm.mean.data_ptr(), norm.std.data_ptr(), vb._states.data_ptr(), vb.capacity)
+           norm.mean.data_ptr(), norm.std.data_ptr(), model.min_log_var.data_ptr(), model.max_log_var.data_ptr(),
+           vb.capacity) + tuple(getattr(vb, f).data_ptr() for f in _VB_FIELDS)
     cache = alg.__dict__.setdefault('_rollout_desc_cache', {})
     hit = cache.get(key)
     if hit is not None:
         return hit
+    if len(cache) >= _ROLLOUT_CACHE_MAX:   # (B, H) or buffers changed: drop the old entries
+        cache.clear()
     L = _lib.lib()
     S, A, C = alg.state_dim, alg.action_dim, alg.con_dim
     pa = [(pg.pview(f'net.{2 * i}.weight')[0], pg.view(f'net.{2 * i}.bias')) for i in range(policy.spec.n_layers)]

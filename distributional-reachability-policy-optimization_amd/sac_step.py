@@ -274,25 +274,32 @@ class SACEngine:
 
     def _actor_arena(self, B):
         """(Re)build the actor exchange arena for batch B: actor grads | safe actor grads |
-        one alpha-loss partial per 16-row tile."""
+        one alpha-loss partial per 16-row tile. Sized once for the solver's batch size
+        (and never below 4096 rows); a larger B re-homes the gradients, which re-points
+        the Parameters' .grad views and drops every cached descriptor and net view (they
+        hold raw pointers into the old arena)."""
         nt = (B + 15) // 16
         if self.actor_xchg is not None and self.alpha_sum.numel() >= nt:
             return
         sol = self.sol
+        nt = max(nt, (max(sol.batch_size, 4096) + 15) // 16)
+        if self.actor_xchg is not None:
+            nt = max(nt, 2 * self.alpha_sum.numel())   # grow geometrically: rare rebuilds
         ga, gs = sol.actor.group, sol.actor_safe.group
         na, ns = ga.size, gs.size
         self.actor_xchg = torch.zeros(na + ns + nt, device=self.dev)
         ga.move_grad(self.actor_xchg[:na], sol.actor)
         gs.move_grad(self.actor_xchg[na:na + ns], sol.actor_safe)
         self.alpha_sum = self.actor_xchg[na + ns:]
-        if hasattr(self, 'desc'):
-            self.desc.pop('a.head', None)
+        self.desc = {}
+        self.nets_view = {}
+        self.B = None          # forces _setup to rebuild the nets over the new gradient views
 
     def _setup(self, B):
         if self.B == B:
             return
-        self.B = B
         self._actor_arena(B)
+        self.B = B
         self.ws = {}
         sol, S, A, C = self.sol, self.S, self.A, self.C
         cg, tg = sol.critic_group, sol.critic_target_group

@@ -498,6 +498,13 @@ int drpo_ens_loss_partials(const float* D, const float* LVR, const float* s, int
                            float weight, const float* gscale, float* mse, float* loss, float* gD, float* gLVR,
                            float* gmin, float* gmax, void* workspace, drpo_ens_reduce_t* reduce_out,
                            drpo_stream_t stream);
+/* The deferred reduction of drpo_ens_loss_partials / drpo_mlp_backward_ens as its own
+ * one-block launch (replaces the reduction step of BatchedGaussianEnsemble.fit,
+ * src/dynamics.py:143-153,163-171): per-member NLL, the step loss and the log-var
+ * bound gradients ACCUMULATED into gmin / gmax (no optimizer step). The member-
+ * sharded fit runs it on a side stream so the bounds' all-reduce overlaps the
+ * members' fused weight-gradient + Adam launch. */
+int drpo_ens_loss_reduce(const drpo_ens_reduce_t* red /* host */, drpo_stream_t stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam (coupled L2), clip_grad_norm_, update_ema (src/ssac.py:446-455,

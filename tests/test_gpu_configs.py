@@ -283,6 +283,38 @@ def test_config_full_width_fit_vs_oracle(c):
         assert not (err > 0).any(), (k, float(np.abs(got - e).max()))
 
 
+def test_fit_head_hidden_layers_2_vs_oracle():
+    """A model with head_hidden_layers=2 (a config option; the reference default is 1)
+    is outside drpo_mlp_backward_ens's shapes: the fit must take the separate NLL launch
+    + generic backward (ensemble_engine.ens_fused_shapes), not raise from the fused one."""
+    from drpo_amd.ensemble_engine import ens_fused_shapes
+    cd = bench.CONFIGS[2]
+    torch.manual_seed(11)
+    alg = bench.make_alg(DEV, 256, cd['H'], cd['E'], 11, bench.ENV_JSON[cd['env']], env=cd['env'],
+                         extra={'model_cfg': {'head_hidden_layers': 2}})
+    m = alg.model_ensemble
+    assert m.head_hidden_layers == 2
+    nets, _ = m.engine._nets(grads=False)
+    assert not ens_fused_shapes(nets, m.state_dim + 1)
+    _fill(alg, cd['env'], 30000, 8)
+    buf = {k: v.cpu() for k, v in alg.replay_buffer.get(as_dict=True).items()}
+    P = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    _oracle_threads()
+    live = O.LiveRNG()
+    ref_losses, ref_elites = O.ens_fit(P, '', {}, buf, 3, m.ensemble_size, m.batch_size, m.holdout_size,
+                                       m.num_elites, live)
+    tape = drpo_amd.TapeNoise(live.entries)
+    losses = m.fit(alg.replay_buffer, steps=3, noise=tape)
+    assert tape.done()
+    np.testing.assert_allclose(losses, ref_losses, rtol=1e-4)
+    assert m._elite_inds == ref_elites
+    sd = m.state_dict()
+    for k in O.ens_param_keys(P, ''):
+        got, e = sd[k].cpu().numpy(), P[k].numpy()
+        err = np.abs(got - e) - (5e-5 + 2e-4 * np.abs(e))
+        assert not (err > 0).any(), (k, float(np.abs(got - e).max()))
+
+
 def _flags_marginal(fns, s2, flags, n_probe=6, rel=1e-5):
     """Rows whose (done, violation) flags flip under +-rel perturbations of next_state:
     there the flag is decided by fp32 rounding, not by the kernel's arithmetic."""

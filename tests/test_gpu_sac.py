@@ -105,3 +105,43 @@ def test_rollout_and_update_matches_reference(env):
                        'n_viol', 'epochs'))
     lq = np.array([x.item() for x in alg.recent_critic_losses])
     np.testing.assert_allclose(lq, d['losses/critic'], rtol=1e-3, atol=1e-5)
+
+
+def test_actor_arena_rebuild_matches_presized_engine():
+    """The actor exchange arena (actor | safe actor grads | alpha-loss partials) is
+    rebuilt when a batch larger than it was sized for arrives: the gradients are
+    re-homed, the Parameters' .grad views follow, and every cached descriptor is
+    dropped. Actor updates at B = 64, 5000 (forces the rebuild), 64 must give bitwise
+    the parameters of an engine whose arena was sized for 8192 rows up front."""
+    from drpo_amd.rng import DeviceNoise
+    d = load_golden('ssac_drpo_quad')
+    env = str(d['meta/env'])
+
+    def run(presize):
+        alg = small_smbpo(d, env)
+        sol = alg.solver
+        sd0 = solver_sd(d, 'sd0/')
+        sol.log_alpha.fill_(float(sd0.pop('log_alpha')))
+        sol.load_state_dict(sd0, strict=False)
+        eng = sol.engine
+        first = eng.actor_xchg
+        if presize:
+            eng._actor_arena(presize)
+        g = torch.Generator().manual_seed(3)
+        noise = DeviceNoise(7)
+        for B in (64, 5000, 64):
+            obs = torch.randn(B, alg.state_dim, generator=g).to(DEV)
+            sol.update_actor_and_alpha(obs, noise=noise)
+        torch.cuda.synchronize()
+        arena = eng.actor_xchg
+        lo, hi = arena.data_ptr(), arena.data_ptr() + 4 * arena.numel()
+        for p in list(sol.actor.parameters()) + list(sol.actor_safe.parameters()):
+            assert p.grad is not None and lo <= p.grad.data_ptr() < hi, 'a .grad view left on the old arena'
+        rebuilt = arena is not first
+        return {k: v.detach().clone() for k, v in sol.state_dict().items()}, rebuilt
+
+    a, rebuilt_a = run(None)
+    b, _ = run(8192)
+    assert rebuilt_a, 'B = 5000 must outgrow the arena sized for the solver batch'
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
