@@ -357,6 +357,8 @@ def main():
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     steady_mode(alg)
+    if os.environ.get('DRPO_BENCH_ELITES'):   # traffic probe: the elite set the rollout draws from
+        alg.model_ensemble._elite_inds = [int(x) for x in os.environ['DRPO_BENCH_ELITES'].split(',')]
     from drpo_amd.distributed import sync_parameters
     sync_parameters(alg)            # every rank starts from rank 0's weights (DP replicas)
     do_sac = not args.rollout_only

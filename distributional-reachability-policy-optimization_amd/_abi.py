@@ -80,6 +80,7 @@ PROTOTYPES = {
     'drpo_event_create': (c_int, [POINTER(c_void_p)]),
     'drpo_event_destroy': (c_int, [P]),
     'drpo_event_record': (c_int, [P, P]),
+    'drpo_stream_wait_event': (c_int, [P, P]),
     'drpo_event_elapsed_ms': (c_int, [POINTER(c_float), P, P]),
     'drpo_grad_sumsq_blocks': (c_int, [c_int64]),
     'drpo_grad_sumsq': (c_int, [P, c_int64, P, P]),

@@ -45,6 +45,18 @@ DRPO_API int drpo_event_record(void* ev, drpo_stream_t stream_) {
   return hipEventRecord((hipEvent_t)ev, stream) == hipSuccess ? DRPO_OK : DRPO_EHIP;
 }
 
+// stream waits for an event recorded on another stream of the same device (the model
+// fit's side stream, ensemble_engine.fit): with the events above, the hand-off costs no
+// system-scope fence
+DRPO_API int drpo_stream_wait_event(drpo_stream_t stream_, void* ev) {
+  const hipError_t r = hipStreamWaitEvent((hipStream_t)stream_, (hipEvent_t)ev, 0);
+  if (r != hipSuccess) {
+    drpo_set_error("hipStreamWaitEvent: %s", hipGetErrorString(r));
+    return DRPO_EHIP;
+  }
+  return DRPO_OK;
+}
+
 DRPO_API int drpo_event_elapsed_ms(float* ms, void* start, void* stop) {
   hipError_t r = hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
   if (r != hipSuccess) {

@@ -31,6 +31,19 @@ constexpr int MAXN = 3;
 
 }  // namespace
 
+// A/B macros of the multi-job forward (profiles/r05/fwd_ab): the first layer's fragments
+// loaded during the input staging (Pre0: measured slower, 48.0 vs 45.6 us per forward
+// launch -- the staging's input loads then wait behind the fragments in the in-order
+// vmcnt, and the first layer did not shorten; off); the policy head one thread per
+// (row, action dim) on the hardware transcendentals (squash_head_tile: 44.9 vs 45.6 us,
+// SAC 66.3 vs 65.6 TFLOP/s; on)
+#ifndef DRPO_FWD_PRE0
+#define DRPO_FWD_PRE0 0
+#endif
+#ifndef DRPO_FWD_HEAD_TILE
+#define DRPO_FWD_HEAD_TILE 1
+#endif
+
 
 // ---------------------------------------------------------------------------
 // forward
@@ -49,6 +62,11 @@ __device__ unsigned long long g_stamps[1 << 16][16];
   } while (0)
 DRPO_API int drpo_debug_stamps(unsigned long long* dst, int n) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * (size_t)n);
+}
+DRPO_API int drpo_debug_stamps_clear() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)) != hipSuccess) return 1;
+  return (int)hipMemset(p, 0, sizeof(g_stamps));
 }
 // backward stamps: rows 32768.. of the same buffer (the forward's slots stay intact)
 #define STAMPW(i)                                                                                 \
@@ -211,15 +229,77 @@ struct MultiArgs {
   uint64_t seed, ctr;
 };
 
+__device__ __forceinline__ GSave layer_save(const drpo_mlp_layer_t& L, int z, int64_t rows, int row0, int nrows) {
+  const size_t so = ((size_t)z * rows + row0) * L.dout;
+  return GSave{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
+}
+
+// A first layer with K <= 16 (one k-step) and more than 16 outputs: its weight
+// fragments and biases are loaded at the top of the workgroup, in flight while the
+// input tile is staged, instead of behind the staging (and its save_x stores, which
+// the first fragment wait would otherwise drain too: vmcnt counts loads and stores in
+// issue order). The first layer was 6-14 k cycles of MFMA-free latency per SAC forward
+// workgroup (profiles/r05/sac_fwd_stamps). Waves owning fewer than FW_MAXC blocks load a
+// clamped duplicate whose results the epilogue discards.
+struct Pre0 {
+  f32x4 w[FW_MAXC];
+  float b[FW_MAXC];
+};
+
+__device__ __forceinline__ void pre0_load(const drpo_mlp_layer_t& L, int z, Pre0& p) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NCB = (L.dout + 15) >> 4;
+  const float* W = L.W + (size_t)z * L.wstride;
+#pragma unroll
+  for (int c = 0; c < FW_MAXC; ++c) p.w[c] = load_pk(W, min(wave + FW_NW * c, NCB - 1), 0, 1);
+  load_bias<FW_NW, FW_MAXC>(L.b + (size_t)z * L.bstride, L.dout, p.b);
+}
+
+template <int ACT, int RB>
+__device__ __forceinline__ void layer_pre0_act(const float* in, const Pre0& p, int N, float* out, const GSave& gs) {
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  f32x4 acc[RB][FW_MAXC], av[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    av[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * LDH + 4 * g);
+#pragma unroll
+    for (int c = 0; c < FW_MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int c = 0; c < FW_MAXC; ++c)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[rb][m], p.w[c][m], acc[rb][c], 0, 0, 0);
+  dense_epilogue<FW_NW, RB, FW_MAXC, ACT>(acc, p.b, N, out, LDH, gs);
+}
+
+// run_layer for a first layer whose fragments were loaded by pre0_load
+template <int RB>
+__device__ __forceinline__ void run_layer_pre0(const float* in, const drpo_mlp_layer_t& __restrict__ L, int z,
+                                               int64_t rows, int row0, int nrows, float* out, const Pre0& p) {
+  const GSave gs = layer_save(L, z, rows, row0, nrows);
+  switch (L.act) {
+    case ACT_RELU: layer_pre0_act<ACT_RELU, RB>(in, p, L.dout, out, gs); break;
+    case ACT_SILU: layer_pre0_act<ACT_SILU, RB>(in, p, L.dout, out, gs); break;
+    case ACT_TANH: layer_pre0_act<ACT_TANH, RB>(in, p, L.dout, out, gs); break;
+    default: layer_pre0_act<ACT_NONE, RB>(in, p, L.dout, out, gs); break;
+  }
+}
+
 template <int RB>
 __device__ __forceinline__ float* run_net_g(const drpo_mlp_fwd_t* __restrict__ a, int ni, float* in, float* bufA,
-                                            float* bufB, int z, int row0, int nrows, float* red) {
+                                            float* bufB, int z, int row0, int nrows, float* red,
+                                            const Pre0* p0 = nullptr) {
   float* cur = in;
   const int nl = a->net[ni].nl;
   for (int l = 0; l < nl; ++l) {
     float* out = (cur == bufA) ? bufB : bufA;
-    run_layer<RB>(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
+    if (l == 0 && p0) run_layer_pre0<RB>(cur, a->net[ni].L[0], z, a->rows, row0, nrows, out, *p0);
+    else run_layer<RB>(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
     lds_barrier();
+    STAMP(2 + l);
     cur = out;
   }
   return cur;
@@ -238,10 +318,6 @@ __device__ __forceinline__ bool heads_pairable(const drpo_mlp_fwd_t* __restrict_
          n1.L[0].act == n2.L[0].act && n1.L[1].act == n2.L[1].act && n1.L[1].dout <= 16 && n2.L[1].dout <= 16;
 }
 
-__device__ __forceinline__ GSave layer_save(const drpo_mlp_layer_t& L, int z, int64_t rows, int row0, int nrows) {
-  const size_t so = ((size_t)z * rows + row0) * L.dout;
-  return GSave{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
-}
 
 template <int RB, int ACT0, int ACT1>
 __device__ __forceinline__ void heads_pair_act(const drpo_mlp_fwd_t* __restrict__ a, const float* T, float* hA,
@@ -255,6 +331,7 @@ __device__ __forceinline__ void heads_pair_act(const drpo_mlp_fwd_t* __restrict_
                                           B0.dout, hB, LDH, layer_save(A0, z, a->rows, row0, nrows),
                                           layer_save(B0, z, a->rows, row0, nrows));
   lds_barrier();
+  STAMP(5);
   tile_dense_narrow_pair<FW_NW, RB, ACT1>(hA, hB, LDH, A0.dout, A1.W + (size_t)z * A1.wstride,
                                           A1.b + (size_t)z * A1.bstride, A1.dout, o, B1.W + (size_t)z * B1.wstride,
                                           B1.b + (size_t)z * B1.bstride, B1.dout, o + 16, LDH, red,
@@ -284,6 +361,51 @@ __device__ __forceinline__ void heads_pair(const drpo_mlp_fwd_t* __restrict__ a,
   }
 }
 
+// The fused squashed-Gaussian head of a policy job (squashed_gaussian_row's arithmetic,
+// src/policy.py:88-97, src/squashed_gaussian.py): one thread per (row, action dim)
+// instead of one per row, on the hardware transcendentals of critic_rows.hpp
+// (DRPO_CRITIC_FAST_MATH; ~1e-6 relative), log(std) taken as the log-std itself (the
+// reference's log(exp(log_std))); the per-dim log-prob terms are summed per row in
+// dimension order through LDS (lpt). The per-row libm chain it replaces was 5.6-8 k
+// cycles at the end of every policy workgroup (profiles/r05/sac_fwd_stamps).
+template <int ROWS>
+__device__ __forceinline__ void squash_head_tile(const float* outp, int row0, int nrows, const drpo_policy_head_t& hd,
+                                                 uint64_t seed, uint64_t ctr, float* lpt) {
+  const int A = hd.A, mode = hd.mode - 1;
+  const int tid = threadIdx.x;
+  if (tid < ROWS * A) {   // ROWS * A <= ROWS * 8 <= FW_NT
+    const int r = tid / A, d = tid - r * A;
+    float term = 0.f;
+    if (r < nrows) {
+      const int64_t i = row0 + r, k = i * A + d;
+      const float* rrow = outp + r * LDH;
+      const float mu = rrow[d];
+      const float ls = -6.f + 10.f * cr_rcp(1.f + cr_exp(-rrow[A + d]));
+      const float sd = cr_exp(ls) * 1.0f;
+      if (hd.amean) gstore(hd.amean + k, DRPO_CRITIC_FAST_MATH ? fast_tanh(mu) : tanhf(mu));
+      if (mode != 2) {
+        const float e = normal_at(hd.eps, k, seed, ctr, hd.site);
+        const float u = (mode == 0) ? e * sd + mu : mu + e * sd;
+        if (hd.a) gstore(hd.a + k, DRPO_CRITIC_FAST_MATH ? fast_tanh(u) : tanhf(u));
+        if (hd.u) gstore(hd.u + k, u);
+        if (hd.e) gstore(hd.e + k, e);
+        const float ladj = 2.f * (0.69314718055994531f - u - cr_softplus(-2.f * u));
+        const float base = -((u - mu) * (u - mu)) * cr_rcp(2.f * (sd * sd)) - ls - 0.91893853320467274f;
+        term = (0.f - ladj) + base;
+      }
+    }
+    lpt[tid] = term;
+  }
+  if (hd.logp && mode != 2) {
+    lds_barrier();
+    if (tid < nrows) {
+      float lp = 0.f;
+      for (int d = 0; d < A; ++d) lp += lpt[tid * A + d];
+      gstore(hd.logp + row0 + tid, lp);
+    }
+  }
+}
+
 template <int RB>
 __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ? 4 : 2, RB == 1 ? 4 : 2))) void mlp_fwd_multi_kernel(MultiArgs m) {
   constexpr int ROWS = 16 * RB;
@@ -300,9 +422,15 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   const int row0 = blockIdx.x * ROWS;
   if (row0 >= a->rows || z >= a->nbatch) return;
   const int nrows = (int)min((int64_t)ROWS, a->rows - row0);
+  STAMP(0);
   const int c0 = a->cols[0], c1 = a->cols[1];
   const int din0 = c0 + c1 + a->cols[2];
   const int kpad = round_up(din0, 16);
+  // the first layer's fragments, in flight during the staging (Pre0)
+  const drpo_mlp_layer_t& L0 = a->net[a->trunk ? 0 : net].L[0];
+  const bool pre0 = DRPO_FWD_PRE0 && din0 <= 16 && L0.dout > 16;
+  Pre0 p0;
+  if (pre0) pre0_load(L0, z, p0);
   for (int e = tid; e < ROWS * kpad; e += FW_NT) {
     const int r = e / kpad, k = e - r * kpad;
     float v = 0.f;
@@ -317,15 +445,18 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
     xin[r * LDH + k] = v;
   }
   lds_barrier();
+  STAMP(1);
+  const Pre0* pp0 = pre0 ? &p0 : nullptr;
   float* outp;
   if (!a->trunk) {
-    outp = run_net_g<RB>(a, net, xin, bA, bB, z, row0, nrows, red);
+    outp = run_net_g<RB>(a, net, xin, bA, bB, z, row0, nrows, red, pp0);
   } else if (heads_pairable(a)) {
     // trunk output stays where the trunk left it; the paired heads use the two
     // other full buffers and write their narrow outputs into xin (consumed)
-    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
+    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red, pp0);
     outp = nullptr;
     heads_pair<RB>(a, t, T, t == bA ? bB : bA, xin, z, row0, nrows, red);
+    STAMP(6);
     if (a->ccb_out) {
       // the constraint critic's upper bound, max over C (drpo_cc_head), from the heads'
       // outputs in LDS (mean head: xin columns 0.., log-std head: columns 16..)
@@ -343,7 +474,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
       }
     }
   } else {
-    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red);
+    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red, pp0);
     const int w = a->net[0].L[a->net[0].nl - 1].dout;
     const int wpad = round_up(w, 16);
     for (int e = tid; e < ROWS * wpad; e += FW_NT) {
@@ -356,11 +487,16 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   }
   // fused squashed-Gaussian head on net 0's output (non-trunk jobs)
   const drpo_policy_head_t& hd = a->head;
-  if (hd.mode != 0 && outp && net == 0 && tid < nrows) {
-    const float* rrow = outp + tid * LDH;
-    squashed_gaussian_row([&](int c) { return rrow[c]; }, (int64_t)(row0 + tid), hd.A, hd.mode - 1, hd.eps, m.seed,
-                          m.ctr, hd.site, hd.a, hd.logp, hd.u, hd.e, hd.amean);
+  if (hd.mode != 0 && outp && net == 0) {
+    if (DRPO_FWD_HEAD_TILE) {
+      squash_head_tile<ROWS>(outp, row0, nrows, hd, m.seed, m.ctr, red);
+    } else if (tid < nrows) {
+      const float* rrow = outp + tid * LDH;
+      squashed_gaussian_row([&](int c) { return rrow[c]; }, (int64_t)(row0 + tid), hd.A, hd.mode - 1, hd.eps, m.seed,
+                            m.ctr, hd.site, hd.a, hd.logp, hd.u, hd.e, hd.amean);
+    }
   }
+  STAMP(15);
 }
 
 DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_mlp_fwd_t* jobs_dev, int njobs,

@@ -417,7 +417,17 @@ class EnsembleEngine:
         stream = _lib.stream()
         # Adam fused into the weight-gradient launch: single process, whole group, no clip
         fuse = self.fused_adam and fused and sh is None and not self.dp.active and len(wl) == 1
-        if fuse:
+        # Member shard: the rank-local members take the same fused weight-
+        # gradient + Adam launch (their tiles of the group's pack map); only the shared
+        # log-var bounds' 2(S+1) gradients leave the step. Their reduction runs as its own
+        # one-block launch on a side stream as soon as the backward has written the NLL
+        # partials; the side stream then sum-all-reduces them (the step's ONE collective)
+        # and steps the bounds, overlapped with the members' launch on the main stream.
+        # The next step's backward (which reads the bounds and rewrites the partials)
+        # waits for it.
+        fuse_sh = self.fused_adam and fused and sh is not None and len(wl) == 1
+        self.fit_path = 'fused' if fuse else ('fused-shard' if fuse_sh else 'separate')   # (tests, probes)
+        if fuse or fuse_sh:
             from ._abi import WgradAdam
             opt = m.optimizer
             opt._ensure_state()
@@ -429,6 +439,19 @@ class EnsembleEngine:
             ad.map, ad.map_host = pm.data_ptr(), ctypes.addressof(pm.host)
             warr, wn = wl[0]
             wws = self._wgrad_ws('fit0', warr, wn)
+        if fuse_sh:
+            bseg = (OptimSeg * 1)(m.optimizer.segment(lo, hi, (0.0, 1.0), zero_grad=True))
+            side = self.__dict__.setdefault('_side', torch.cuda.Stream(device=self.dev))
+            if getattr(self, '_side_evs', None) is None:   # fence-free library events (csrc/core.hip)
+                self._side_evs = []
+                for _ in range(2):
+                    e = ctypes.c_void_p()
+                    _lib.check(L.drpo_event_create(ctypes.byref(e)), 'event_create')
+                    self._side_evs.append(e)
+            ev_bwd, ev_done = self._side_evs
+            main_s = stream
+            side_s = ctypes.c_void_p(side.cuda_stream)
+            pending = False
         gargs = [_lib.ptr(rb._states), _lib.ptr(rb._actions), _lib.ptr(rb._next_states), _lib.ptr(rb._rewards),
                  ptr_host, _lib.ptr(ptr_dev), rb.capacity, rows]
         loss_base = losses.data_ptr()
@@ -455,6 +478,8 @@ class EnsembleEngine:
             up.s, up.t = fd.src[0], ct.data_ptr() + 4 * k * rows * S1
             red_in.loss = loss_base + 4 * i
             _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
+            if fuse_sh and pending:           # the previous step's bounds are stepped
+                _lib.check(L.drpo_stream_wait_event(main_s, ev_done), 'stream_wait_event')
             if fused:
                 _lib.check(L.drpo_mlp_backward_ens(ctypes.byref(bd), ctypes.byref(up), ctypes.byref(red_in),
                                                    ctypes.byref(red), stream), 'ensemble backward')
@@ -469,6 +494,21 @@ class EnsembleEngine:
                 _lib.check(L.drpo_mlp_wgrad_adam(warr, wn, ctypes.byref(red), ctypes.byref(ad), wws.data_ptr(),
                                                  wws.numel(), stream), 'ensemble wgrad + adam')
                 continue
+            if fuse_sh:
+                lr_bc1, bc2 = m.optimizer.step_scalars()
+                _lib.check(L.drpo_event_record(ev_bwd, main_s), 'event_record')
+                _lib.check(L.drpo_stream_wait_event(side_s, ev_bwd), 'stream_wait_event')
+                _lib.check(L.drpo_ens_loss_reduce(ctypes.byref(red), side_s), 'ens_loss_reduce')
+                with torch.cuda.stream(side):      # the collective on the side stream
+                    sh.sum_(bounds_grad)
+                bseg[0].lr_over_bc1, bseg[0].bc2_sqrt = lr_bc1, bc2
+                _lib.check(L.drpo_optim_step(bseg, 1, side_s), 'optim_step (log-var bounds)')
+                _lib.check(L.drpo_event_record(ev_done, side_s), 'event_record')
+                pending = True
+                ad.lr_over_bc1, ad.bc2_sqrt = lr_bc1, bc2
+                _lib.check(L.drpo_mlp_wgrad_adam(warr, wn, None, ctypes.byref(ad), wws.data_ptr(), wws.numel(),
+                                                 stream), 'ensemble wgrad + adam (member shard)')
+                continue
             # the loss reduction rides as the last workgroup of the wgrad launch
             self._wgrad('fit', wl, red, stream)
             if sh is None:
@@ -481,6 +521,8 @@ class EnsembleEngine:
                 for k in range(len(arr)):
                     arr[k].lr_over_bc1, arr[k].bc2_sqrt = lr_bc1, bc2
                 _lib.check(L.drpo_optim_step(arr, len(arr), stream), 'optim_step')
+        if fuse_sh and pending:
+            _lib.check(L.drpo_stream_wait_event(main_s, ev_done), 'stream_wait_event')
         # holdout: the same rows for every member (src/dynamics.py:175-183)
         hb = m.holdout_size
         assert hb == b, 'reference asserts holdout_size == batch_size (src/dynamics.py:177)'

@@ -48,6 +48,7 @@ int drpo_event_create(void** ev);
 int drpo_event_destroy(void* ev);
 int drpo_event_record(void* ev, drpo_stream_t stream);
 int drpo_event_elapsed_ms(float* ms /* host */, void* start, void* stop);
+int drpo_stream_wait_event(drpo_stream_t stream, void* ev);   /* hipStreamWaitEvent (cross-stream hand-off) */
 
 /* ---------------------------------------------------------------- rollout
  * Replaces SMBPO.rollout (src/smbpo.py:229-249) together with

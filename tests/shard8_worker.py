@@ -63,8 +63,14 @@ def main():
                     m.group.view(key)[sh.z0:sh.z1].copy_(m.group.view(key, ref0)[sh.z0:sh.z1])
         for key in ('min_log_var', 'max_log_var'):
             m.group.view(key).copy_(m.group.view(key, ref0))
+    from drpo_amd.distributed import CommLog
+    c0 = CommLog.calls
     losses = m.fit(alg.replay_buffer, steps=3, noise=drpo_amd.TapeNoise(tape(3, len(alg.replay_buffer), 8 * 256, 256)))
     torch.cuda.synchronize()
+    # the fused member-shard step (ensemble_engine.fit): ONE all-reduce per fit step (the
+    # log-var bounds' gradients) + the per-step loss vector's sum after the fit
+    assert m.engine.fit_path == 'fused-shard', m.engine.fit_path
+    assert CommLog.calls - c0 == 3 + 1, CommLog.calls - c0
     ref = np.load(out_path)
     np.testing.assert_allclose(losses, ref['losses'], rtol=1e-5)
     assert m._elite_inds == list(ref['elites']), (m._elite_inds, ref['elites'])
