@@ -136,7 +136,8 @@ class MlpFwd(ctypes.Structure):
     _fields_ = [('src', P * 3), ('cols', c_int * 3), ('ld', c_int * 3), ('sstride', c_int64 * 3),
                 ('nmean', P), ('nstd', P), ('save_x', P), ('net', MlpNet * 3), ('nnets', c_int), ('trunk', c_int),
                 ('rows', c_int64), ('nbatch', c_int), ('head', PolicyHead), ('split_heads', c_int),
-                ('ccb_out', P), ('ccb_dist', c_int), ('ccb_ratio', c_float), ('ccb_lmin', c_float), ('ccb_lmax', c_float)]
+                ('ccb_out', P), ('ccb_dist', c_int), ('ccb_ratio', c_float), ('ccb_lmin', c_float), ('ccb_lmax', c_float),
+                ('pair', c_int), ('head2', PolicyHead), ('pre', MlpNet), ('pre_head', PolicyHead)]
 
 
 class MlpBwdLayer(ctypes.Structure):

@@ -339,8 +339,8 @@ __device__ __forceinline__ float swz_pick(const f32x4& v, int r, int g) {
 
 template <int NW, int RB, int MAXC, int ACT>
 __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], const float (&bvs)[MAXC], int N,
-                                               float* out, int ldo, const GSave& gs) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                               float* out, int ldo, const GSave& gs, int wv = -1) {
+  const int lane = threadIdx.x & 63, wave = wv >= 0 ? wv : (int)(threadIdx.x >> 6);
   const int l15 = lane & 15, g = lane >> 4;
   const int NB = (N + 15) >> 4;
 #pragma unroll
@@ -463,13 +463,16 @@ __device__ __forceinline__ void tile_dense_mma(const float* in, int ldi, const f
   }
 }
 
-template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0>
+// wv >= 0: the wave index within a sub-group of NW waves (a workgroup split into halves
+// that run different layers, e.g. pair_nets); RING > 0: the weight ring depth
+template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0, int RING = 0>
 __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,
-                                                const GSave& gs, const float* Pl = nullptr) {
+                                                const GSave& gs, const float* Pl = nullptr, int wv = -1) {
   static_assert(NL == 0 || NK > 0, "LDS-resident k-steps need the unrolled core");
+  static_assert(RING == 0 || NK > 0, "a ring depth needs the unrolled core");
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = wv >= 0 ? wv : (int)(tid >> 6);
   const int l15 = lane & 15, g = lane >> 4;
   const int NKS = NK > 0 ? NK : (K + 15) >> 4;
   int cbs[MAXC];
@@ -482,14 +485,22 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int PF = NK > 0 ? pf_depth<MAXC>() : PF_D;
+  constexpr int PF = RING > 0 ? RING : (NK > 0 ? pf_depth<MAXC>() : PF_D);
   f32x4 bq[PF][MAXC];
 #pragma unroll
   for (int u = 0; u < PF - 1; ++u)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) bq[u][c] = load_frag<NL>(P, Pl, cbs[c], min(u, NKS - 1), NKS);
   float bvs[MAXC];
-  load_bias<NW, MAXC>(bias, N, bvs);
+  if (wv >= 0) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int col = cbs[c] * 16 + l15;
+      bvs[c] = (bias && col < N) ? gload(bias + col) : 0.f;
+    }
+  } else {
+    load_bias<NW, MAXC>(bias, N, bvs);
+  }
 
   if constexpr (NK > 0) {
     f32x4 an[RB], ac[RB];
@@ -543,7 +554,7 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
       }
     }
   }
-  dense_epilogue<NW, RB, MAXC, ACT>(acc, bvs, N, out, ldo, gs);
+  dense_epilogue<NW, RB, MAXC, ACT>(acc, bvs, N, out, ldo, gs, wv);
 }
 
 // Wave w owns column blocks w, w+NW, ... < NCB: when NW does not divide NCB (13

@@ -31,15 +31,11 @@ constexpr int MAXN = 3;
 
 }  // namespace
 
-// A/B macros of the multi-job forward (profiles/r05/fwd_ab): the first layer's fragments
-// loaded during the input staging (Pre0: measured slower, 48.0 vs 45.6 us per forward
-// launch -- the staging's input loads then wait behind the fragments in the in-order
-// vmcnt, and the first layer did not shorten; off); the policy head one thread per
-// (row, action dim) on the hardware transcendentals (squash_head_tile: 44.9 vs 45.6 us,
-// SAC 66.3 vs 65.6 TFLOP/s; on)
-#ifndef DRPO_FWD_PRE0
-#define DRPO_FWD_PRE0 0
-#endif
+// A/B macro of the multi-job forward (profiles/r05/fwd_ab): the policy head one thread
+// per (row, action dim) on the hardware transcendentals (squash_head_tile: 44.9 vs
+// 45.6 us per forward launch, SAC 66.3 vs 65.6 TFLOP/s). (Measured and removed: the
+// first layer's fragments loaded during the input staging, 48.0 vs 45.6 us: the
+// staging's input loads then wait behind the fragments in the in-order vmcnt.)
 #ifndef DRPO_FWD_HEAD_TILE
 #define DRPO_FWD_HEAD_TILE 1
 #endif
@@ -234,70 +230,14 @@ __device__ __forceinline__ GSave layer_save(const drpo_mlp_layer_t& L, int z, in
   return GSave{L.sy ? L.sy + so : nullptr, L.sz ? L.sz + so : nullptr, L.dout, nrows};
 }
 
-// A first layer with K <= 16 (one k-step) and more than 16 outputs: its weight
-// fragments and biases are loaded at the top of the workgroup, in flight while the
-// input tile is staged, instead of behind the staging (and its save_x stores, which
-// the first fragment wait would otherwise drain too: vmcnt counts loads and stores in
-// issue order). The first layer was 6-14 k cycles of MFMA-free latency per SAC forward
-// workgroup (profiles/r05/sac_fwd_stamps). Waves owning fewer than FW_MAXC blocks load a
-// clamped duplicate whose results the epilogue discards.
-struct Pre0 {
-  f32x4 w[FW_MAXC];
-  float b[FW_MAXC];
-};
-
-__device__ __forceinline__ void pre0_load(const drpo_mlp_layer_t& L, int z, Pre0& p) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int NCB = (L.dout + 15) >> 4;
-  const float* W = L.W + (size_t)z * L.wstride;
-#pragma unroll
-  for (int c = 0; c < FW_MAXC; ++c) p.w[c] = load_pk(W, min(wave + FW_NW * c, NCB - 1), 0, 1);
-  load_bias<FW_NW, FW_MAXC>(L.b + (size_t)z * L.bstride, L.dout, p.b);
-}
-
-template <int ACT, int RB>
-__device__ __forceinline__ void layer_pre0_act(const float* in, const Pre0& p, int N, float* out, const GSave& gs) {
-  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
-  f32x4 acc[RB][FW_MAXC], av[RB];
-#pragma unroll
-  for (int rb = 0; rb < RB; ++rb) {
-    av[rb] = *reinterpret_cast<const f32x4*>(in + (rb * 16 + l15) * LDH + 4 * g);
-#pragma unroll
-    for (int c = 0; c < FW_MAXC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int c = 0; c < FW_MAXC; ++c)
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-        acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[rb][m], p.w[c][m], acc[rb][c], 0, 0, 0);
-  dense_epilogue<FW_NW, RB, FW_MAXC, ACT>(acc, p.b, N, out, LDH, gs);
-}
-
-// run_layer for a first layer whose fragments were loaded by pre0_load
 template <int RB>
-__device__ __forceinline__ void run_layer_pre0(const float* in, const drpo_mlp_layer_t& __restrict__ L, int z,
-                                               int64_t rows, int row0, int nrows, float* out, const Pre0& p) {
-  const GSave gs = layer_save(L, z, rows, row0, nrows);
-  switch (L.act) {
-    case ACT_RELU: layer_pre0_act<ACT_RELU, RB>(in, p, L.dout, out, gs); break;
-    case ACT_SILU: layer_pre0_act<ACT_SILU, RB>(in, p, L.dout, out, gs); break;
-    case ACT_TANH: layer_pre0_act<ACT_TANH, RB>(in, p, L.dout, out, gs); break;
-    default: layer_pre0_act<ACT_NONE, RB>(in, p, L.dout, out, gs); break;
-  }
-}
-
-template <int RB>
-__device__ __forceinline__ float* run_net_g(const drpo_mlp_fwd_t* __restrict__ a, int ni, float* in, float* bufA,
-                                            float* bufB, int z, int row0, int nrows, float* red,
-                                            const Pre0* p0 = nullptr) {
+__device__ __forceinline__ float* run_net_g(const drpo_mlp_net_t& __restrict__ n, int64_t rows, float* in, float* bufA,
+                                            float* bufB, int z, int row0, int nrows, float* red) {
   float* cur = in;
-  const int nl = a->net[ni].nl;
+  const int nl = n.nl;
   for (int l = 0; l < nl; ++l) {
     float* out = (cur == bufA) ? bufB : bufA;
-    if (l == 0 && p0) run_layer_pre0<RB>(cur, a->net[ni].L[0], z, a->rows, row0, nrows, out, *p0);
-    else run_layer<RB>(cur, LDH, a->net[ni].L[l], z, a->rows, row0, nrows, out, red);
+    run_layer<RB>(cur, LDH, n.L[l], z, rows, row0, nrows, out, red);
     lds_barrier();
     STAMP(2 + l);
     cur = out;
@@ -370,7 +310,7 @@ __device__ __forceinline__ void heads_pair(const drpo_mlp_fwd_t* __restrict__ a,
 // cycles at the end of every policy workgroup (profiles/r05/sac_fwd_stamps).
 template <int ROWS>
 __device__ __forceinline__ void squash_head_tile(const float* outp, int row0, int nrows, const drpo_policy_head_t& hd,
-                                                 uint64_t seed, uint64_t ctr, float* lpt) {
+                                                 uint64_t seed, uint64_t ctr, float* lpt, float* a_lds = nullptr) {
   const int A = hd.A, mode = hd.mode - 1;
   const int tid = threadIdx.x;
   if (tid < ROWS * A) {   // ROWS * A <= ROWS * 8 <= FW_NT
@@ -386,7 +326,9 @@ __device__ __forceinline__ void squash_head_tile(const float* outp, int row0, in
       if (mode != 2) {
         const float e = normal_at(hd.eps, k, seed, ctr, hd.site);
         const float u = (mode == 0) ? e * sd + mu : mu + e * sd;
-        if (hd.a) gstore(hd.a + k, DRPO_CRITIC_FAST_MATH ? fast_tanh(u) : tanhf(u));
+        const float act = DRPO_CRITIC_FAST_MATH ? fast_tanh(u) : tanhf(u);
+        if (hd.a) gstore(hd.a + k, act);
+        if (a_lds) a_lds[r * LDH + d] = act;   // chain: the action as the next net's input columns
         if (hd.u) gstore(hd.u + k, u);
         if (hd.e) gstore(hd.e + k, e);
         const float ladj = 2.f * (0.69314718055994531f - u - cr_softplus(-2.f * u));
@@ -404,6 +346,60 @@ __device__ __forceinline__ void squash_head_tile(const float* outp, int row0, in
       gstore(hd.logp + row0 + tid, lp);
     }
   }
+}
+
+// A pair job (drpo_mlp_fwd_t.pair): two 3-layer ReLU nets of one shape on the same input
+// -- the twin critics, the actor and the safe actor -- run by ONE workgroup: waves 0-3
+// run net 0's layers, waves 4-7 net 1's (4 column blocks each of a 256-wide layer, so
+// every SIMD carries one wave of each net: balanced), the narrow output layers as one
+// split-K pair. One staging and one chain of three phases instead of two workgroups each
+// staging the input and running three phases (forward stamps: staging + first layer +
+// narrow layer are ~15-20 k cycles of each such workgroup, profiles/r05/sac_fwd_stamps).
+// Buffers: in -> (bA, bB) -> (in, T) -> bA columns [0, 16) (net 0) and [16, 32) (net 1).
+template <int RB, int NK0>
+__device__ __forceinline__ void pair_nets_nk(const drpo_mlp_net_t& A, const drpo_mlp_net_t& B, int64_t rows, float* in,
+                                             float* bA, float* bB, float* T, int z, int row0, int nrows, float* red) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool second = wave >= FW_NW / 2;
+  const int wl = second ? wave - FW_NW / 2 : wave;
+  const drpo_mlp_net_t& N = second ? B : A;
+  auto W = [&](const drpo_mlp_layer_t& L) { return L.W + (size_t)z * L.wstride; };
+  auto bb = [&](const drpo_mlp_layer_t& L) { return L.b + (size_t)z * L.bstride; };
+  const drpo_mlp_layer_t &L0 = N.L[0], &L1 = N.L[1];
+  tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, NK0, 0, 2>(in, LDH, L0.din, W(L0), bb(L0), L0.dout, second ? bB : bA,
+                                                         LDH, layer_save(L0, z, rows, row0, nrows), nullptr, wl);
+  lds_barrier();
+  STAMP(2);
+  tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, 16, 0, 2>(second ? bB : bA, LDH, 256, W(L1), bb(L1), L1.dout,
+                                                        second ? T : in, LDH, layer_save(L1, z, rows, row0, nrows),
+                                                        nullptr, wl);
+  lds_barrier();
+  STAMP(3);
+  const drpo_mlp_layer_t &A2 = A.L[2], &B2 = B.L[2];
+  tile_dense_narrow_pair<FW_NW, RB, ACT_NONE>(in, T, LDH, A2.din, W(A2), bb(A2), A2.dout, bA, W(B2), bb(B2), B2.dout,
+                                              bA + 16, LDH, red, layer_save(A2, z, rows, row0, nrows),
+                                              layer_save(B2, z, rows, row0, nrows));
+  lds_barrier();
+  STAMP(4);
+}
+
+template <int RB>
+__device__ __forceinline__ void pair_nets(const drpo_mlp_net_t& A, const drpo_mlp_net_t& B, int64_t rows, float* in,
+                                          float* bA, float* bB, float* T, int z, int row0, int nrows, float* red) {
+  if (A.L[0].din <= 16) pair_nets_nk<RB, 1>(A, B, rows, in, bA, bB, T, z, row0, nrows, red);
+  else pair_nets_nk<RB, 4>(A, B, rows, in, bA, bB, T, z, row0, nrows, red);
+}
+
+// host-side shape check of a pair job (the kernel's pair_nets assumptions)
+static int pair_ok(const drpo_mlp_fwd_t* a) {
+  if (a->trunk || a->nnets != 2) return 0;
+  const drpo_mlp_net_t &A = a->net[0], &B = a->net[1];
+  if (A.nl != 3 || B.nl != 3) return 0;
+  for (int l = 0; l < 3; ++l)
+    if (A.L[l].din != B.L[l].din || A.L[l].dout != B.L[l].dout || A.L[l].act != B.L[l].act) return 0;
+  const int k0 = (A.L[0].din + 15) >> 4;
+  return (k0 == 1 || k0 == 4) && A.L[0].dout == 256 && A.L[1].din == 256 && A.L[1].dout == 256 &&
+         A.L[2].dout <= 16 && A.L[0].act == ACT_RELU && A.L[1].act == ACT_RELU && A.L[2].act == ACT_NONE;
 }
 
 template <int RB>
@@ -426,11 +422,8 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   const int c0 = a->cols[0], c1 = a->cols[1];
   const int din0 = c0 + c1 + a->cols[2];
   const int kpad = round_up(din0, 16);
-  // the first layer's fragments, in flight during the staging (Pre0)
-  const drpo_mlp_layer_t& L0 = a->net[a->trunk ? 0 : net].L[0];
-  const bool pre0 = DRPO_FWD_PRE0 && din0 <= 16 && L0.dout > 16;
-  Pre0 p0;
-  if (pre0) pre0_load(L0, z, p0);
+  // chain jobs: the src[1] block (the action) comes from the pre net's head below
+  const bool chain = a->pre.nl > 0;
   for (int e = tid; e < ROWS * kpad; e += FW_NT) {
     const int r = e / kpad, k = e - r * kpad;
     float v = 0.f;
@@ -438,7 +431,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
       const int64_t row = row0 + r;
       const int q = k < c0 ? 0 : (k - c0 < c1 ? 1 : 2);
       const int kk = q == 0 ? k : (q == 1 ? k - c0 : k - c0 - c1);
-      v = a->src[q][(size_t)z * a->sstride[q] + row * a->ld[q] + kk];
+      if (!(chain && q == 1)) v = a->src[q][(size_t)z * a->sstride[q] + row * a->ld[q] + kk];
       if (q == 0 && a->nmean) v = (v - a->nmean[kk]) / (a->nstd[kk] + 1e-6f);
       if (a->save_x) a->save_x[((size_t)z * a->rows + row) * din0 + k] = v;
     }
@@ -446,14 +439,27 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   }
   lds_barrier();
   STAMP(1);
-  const Pre0* pp0 = pre0 ? &p0 : nullptr;
+  if (chain) {
+    // the policy on the src[0] columns (its first layer reads the input tile's first K
+    // columns; the weights are zero beyond its own K), its sampled action into the input
+    // tile's src[1] columns
+    const float* po = run_net_g<RB>(a->pre, a->rows, xin, bA, bB, z, row0, nrows, red);
+    squash_head_tile<ROWS>(po, row0, nrows, a->pre_head, m.seed, m.ctr, red, xin + c0);
+    lds_barrier();
+    STAMP(7);
+  }
   float* outp;
-  if (!a->trunk) {
-    outp = run_net_g<RB>(a, net, xin, bA, bB, z, row0, nrows, red, pp0);
+  float* outp2 = nullptr;
+  if (a->pair) {
+    pair_nets<RB>(a->net[0], a->net[1], a->rows, xin, bA, bB, T, z, row0, nrows, red);
+    outp = bA;
+    outp2 = bA + 16;
+  } else if (!a->trunk) {
+    outp = run_net_g<RB>(a->net[net], a->rows, xin, bA, bB, z, row0, nrows, red);
   } else if (heads_pairable(a)) {
     // trunk output stays where the trunk left it; the paired heads use the two
     // other full buffers and write their narrow outputs into xin (consumed)
-    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red, pp0);
+    float* t = run_net_g<RB>(a->net[0], a->rows, xin, bA, bB, z, row0, nrows, red);
     outp = nullptr;
     heads_pair<RB>(a, t, T, t == bA ? bB : bA, xin, z, row0, nrows, red);
     STAMP(6);
@@ -474,7 +480,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
       }
     }
   } else {
-    float* t = run_net_g<RB>(a, 0, xin, bA, bB, z, row0, nrows, red, pp0);
+    float* t = run_net_g<RB>(a->net[0], a->rows, xin, bA, bB, z, row0, nrows, red);
     const int w = a->net[0].L[a->net[0].nl - 1].dout;
     const int wpad = round_up(w, 16);
     for (int e = tid; e < ROWS * wpad; e += FW_NT) {
@@ -483,9 +489,10 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
     }
     lds_barrier();
     outp = nullptr;
-    for (int h = 1; h < a->nnets; ++h) run_net_g<RB>(a, h, T, bA, bB, z, row0, nrows, red);
+    for (int h = 1; h < a->nnets; ++h) run_net_g<RB>(a->net[h], a->rows, T, bA, bB, z, row0, nrows, red);
   }
-  // fused squashed-Gaussian head on net 0's output (non-trunk jobs)
+  // fused squashed-Gaussian heads on net 0's output (non-trunk jobs) and, for a pair
+  // job, on net 1's (head2; its log-prob scratch after head's)
   const drpo_policy_head_t& hd = a->head;
   if (hd.mode != 0 && outp && net == 0) {
     if (DRPO_FWD_HEAD_TILE) {
@@ -496,6 +503,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
                             m.ctr, hd.site, hd.a, hd.logp, hd.u, hd.e, hd.amean);
     }
   }
+  if (outp2 && a->head2.mode != 0) squash_head_tile<ROWS>(outp2, row0, nrows, a->head2, m.seed, m.ctr, red + ROWS * 8);
   STAMP(15);
 }
 
@@ -527,8 +535,27 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
         DRPO_REQUIRE(check_net(a->net[h], din0), "drpo_mlp_forward_multi: job %d bad net %d", j, h);
     }
     if (a->head.mode != 0)
-      DRPO_REQUIRE(a->head.mode <= 3 && a->head.A >= 1 && 2 * a->head.A == a->net[0].L[a->net[0].nl - 1].dout,
+      DRPO_REQUIRE(a->head.mode <= 3 && a->head.A >= 1 && a->head.A <= 8 &&
+                       2 * a->head.A == a->net[0].L[a->net[0].nl - 1].dout,
                    "drpo_mlp_forward_multi: job %d policy head shape", j);
+    if (a->pair) {
+      DRPO_REQUIRE(pair_ok(a), "drpo_mlp_forward_multi: job %d: a pair job needs two 3-layer ReLU nets of one shape "
+                               "[K <= 16 or 49..64 -> 256 -> 256 -> <= 16]", j);
+      if (a->head2.mode != 0)
+        DRPO_REQUIRE(a->head2.mode <= 3 && a->head2.A >= 1 && a->head2.A <= 8 &&
+                         2 * a->head2.A == a->net[1].L[2].dout,
+                     "drpo_mlp_forward_multi: job %d second policy head shape", j);
+    } else {
+      DRPO_REQUIRE(a->head2.mode == 0, "drpo_mlp_forward_multi: job %d: head2 needs a pair job", j);
+    }
+    if (a->pre.nl > 0) {
+      const drpo_mlp_net_t& pn = a->pre;
+      DRPO_REQUIRE(check_net(pn, a->cols[0]) && (a->pre_head.mode == 1 || a->pre_head.mode == 2) &&
+                       a->pre_head.A == a->cols[1] && a->pre_head.A >= 1 && a->pre_head.A <= 8 &&
+                       2 * a->pre_head.A == pn.L[pn.nl - 1].dout && !a->save_x && !a->nmean,
+                   "drpo_mlp_forward_multi: job %d: a chain needs a policy net on the src[0] columns whose sampled "
+                   "action is the src[1] block (no input save / normalizer)", j);
+    }
     if (a->ccb_out) {   // the same conditions as heads_pairable (device side)
       const drpo_mlp_net_t &n1 = a->net[1], &n2 = a->net[2];
       DRPO_REQUIRE(a->trunk && a->nnets == 3 && n1.nl == 2 && n2.nl == 2 && n1.L[0].din == 256 &&
@@ -536,7 +563,7 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
                        n1.L[1].act == n2.L[1].act && n1.L[1].dout <= 16 && n2.L[1].dout <= 16,
                    "drpo_mlp_forward_multi: job %d: the constraint bound needs a trunk job with paired heads", j);
     }
-    const int ns = a->trunk ? 1 : a->nnets;
+    const int ns = (a->trunk || a->pair) ? 1 : a->nnets;
     DRPO_REQUIRE(slots + ns <= MJ_MAXSLOT, "drpo_mlp_forward_multi: too many nets");
     for (int h = 0; h < ns; ++h) {
       m.slot_job[slots] = (unsigned char)j;

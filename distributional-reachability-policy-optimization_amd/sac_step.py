@@ -72,8 +72,19 @@ def noise_tag(eps):
     return '.p' if eps is not None else '.d'
 
 
+def fill_net(dst, net, wstride=None):
+    """drpo_mlp_net_t of a Net (layers, save buffers, per-member strides)."""
+    dst.nl = len(net.layers)
+    for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
+        L = dst.L[l]
+        L.W, L.b, L.din, L.dout, L.act = W.data_ptr(), b.data_ptr(), din, dout, act
+        L.sy, L.sz = _p(net.sy[l]), _p(net.sz[l])
+        L.wstride, L.bstride = (0, 0) if wstride is None else wstride[l]
+
+
 def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, wstride=None, sstride=None,
-             split_heads=False):
+             split_heads=False, pair=False):
+    """pair: the two nets run by one workgroup (multi-job launches; drpo_mlp_fwd_t.pair)."""
     d = MlpFwd()
     for k, (t, cols) in enumerate(srcs):
         d.src[k] = _p(t)
@@ -83,14 +94,33 @@ def fill_fwd(nets, srcs, rows, trunk=False, save_x=None, norm=None, nbatch=1, ws
     d.nmean, d.nstd = (norm[0].data_ptr(), norm[1].data_ptr()) if norm is not None else (0, 0)
     d.save_x = _p(save_x)
     for j, net in enumerate(nets):
-        d.net[j].nl = len(net.layers)
-        for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
-            L = d.net[j].L[l]
-            L.W, L.b, L.din, L.dout, L.act = W.data_ptr(), b.data_ptr(), din, dout, act
-            L.sy, L.sz = _p(net.sy[l]), _p(net.sz[l])
-            L.wstride, L.bstride = (0, 0) if wstride is None else wstride[j][l]
+        fill_net(d.net[j], net, None if wstride is None else wstride[j])
     d.nnets, d.trunk, d.rows, d.nbatch = len(nets), int(trunk), rows, nbatch
     d.split_heads = int(split_heads)
+    d.pair = int(pair)
+    return d
+
+
+def pairable(a, b):
+    """Two nets one pair job can run (csrc/mlp.hip pair_ok): 3-layer ReLU nets of one shape
+    [K <= 16 or 49..64 -> 256 -> 256 -> <= 16] (the reference's default widths)."""
+    la, lb = a.layers, b.layers
+    if len(la) != 3 or len(lb) != 3:
+        return False
+    if any(x[2:5] != y[2:5] for x, y in zip(la, lb)):
+        return False
+    (_, _, k0, n0, a0, _), (_, _, k1, n1, a1, _), (_, _, _, n2, a2, _) = la
+    return ((k0 + 15) // 16 in (1, 4) and n0 == 256 and k1 == 256 and n1 == 256 and n2 <= 16 and
+            a0 == ACT_ID['relu'] and a1 == ACT_ID['relu'] and a2 == 0)
+
+
+def with_pre(d, policy, mode, A, eps, site, logp=None):
+    """Chain (drpo_mlp_fwd_t.pre): the policy runs first in the same workgroup on the
+    src[0] columns; its sampled action (mode 1 sample / 2 rsample) is the job's src[1]
+    block, straight from LDS."""
+    fill_net(d.pre, policy)
+    h = d.pre_head
+    h.mode, h.A, h.eps, h.site, h.logp = mode, A, _p(eps), site, _p(logp)
     return d
 
 
@@ -127,9 +157,10 @@ def fill_bwd(nets, gouts, rows, trunk=False, dx=None, nbatch=1, wstride=None, sp
 HEAD_SAMPLE, HEAD_RSAMPLE, HEAD_MEAN = 1, 2, 3
 
 
-def with_head(d, mode, A, eps, site, a=None, logp=None, u=None, e=None, amean=None):
-    """Attach a fused squashed-Gaussian head (drpo_policy_head_t) to a forward descriptor."""
-    h = d.head
+def with_head(d, mode, A, eps, site, a=None, logp=None, u=None, e=None, amean=None, second=False):
+    """Attach a fused squashed-Gaussian head (drpo_policy_head_t) to a forward descriptor
+    (second: the head of a pair job's net 1, drpo_mlp_fwd_t.head2)."""
+    h = d.head2 if second else d.head
     h.mode, h.A, h.eps, h.site = mode, A, _p(eps), site
     h.a, h.logp, h.u, h.e, h.amean = _p(a), _p(logp), _p(u), _p(e), _p(amean)
     return d
@@ -171,11 +202,12 @@ def wgrad_workspace(cache, key, arr, n, dev):
 
 
 def fwd_flops(d):
-    """Algorithmic FLOPs of one drpo_mlp_forward launch (2 * rows * sum din*dout)."""
+    """Algorithmic FLOPs of one drpo_mlp_forward launch (2 * rows * sum din*dout), the
+    chained policy of a multi-job launch included."""
     macs = 0
-    for j in range(d.nnets):
-        for l in range(d.net[j].nl):
-            macs += d.net[j].L[l].din * d.net[j].L[l].dout
+    for n in [d.net[j] for j in range(d.nnets)] + [d.pre]:
+        for l in range(n.nl):
+            macs += n.L[l].din * n.L[l].dout
     return 2 * d.rows * d.nbatch * macs
 
 
@@ -567,22 +599,21 @@ class SACEngine:
                                                   self.buf('c.hm', B, C).data_ptr(), _lib.stream()),
                            'env_constraints')
         xs = self.buf('c.x', B, S + A)
-        a2, lp2, a2s = self.buf('c.a2', B, A), self.buf('c.lp2', B), self.buf('c.a2s', B, A)
-        # launch 1: a' ~ pi(s') with log pi, a'_safe ~ pi_safe(s') (robust: model s'), and
-        # the twin critics + constraint critic at (s, a) with their backward saves
-        # (jobs are ordered longest chain first: workgroups dispatch in slot order, so the
-        # short chains fill the tail instead of leaving the long ones running alone)
-        self._run_multi('c.f1' + rk + noise_tag(e1), lambda: [
+        lp2 = self.buf('c.lp2', B)
+        # ONE launch (jobs longest chain first: workgroups dispatch in slot order, so the
+        # short chains fill the tail): the constraint critic and the twin critics (one
+        # workgroup for both twins) at (s, a) with their backward saves, and the targets with
+        # their next-state policies chained in (drpo_mlp_fwd_t.pre): a'_safe ~ pi_safe(s')
+        # (robust: the model's s') -> target certificate at (s', a'_safe); a' ~ pi(s') with
+        # log pi -> target twins at (s', a') (src/ssac.py:284-294,304-400)
+        pq = pairable(n['q0'], n['q1'])
+        self._run_multi('c.f' + rk + noise_tag(e1), lambda: [
+            with_pre(fill_fwd(self._cc_nets('t'), [(s2c, S), (None, A), (None, 0)], B, trunk=True),
+                     Net(n['safe'].layers), HEAD_SAMPLE, A, e2, SITE_SAFE_NEXT),
+            with_pre(fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (None, A), (None, 0)], B, pair=pq),
+                     Net(n['actor'].layers), HEAD_SAMPLE, A, e1, SITE_PI_NEXT, logp=lp2),
             fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
-            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs),
-            with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs2, S), (None, 0), (None, 0)], B), HEAD_SAMPLE, A,
-                      e1, SITE_PI_NEXT, a=a2, logp=lp2),
-            with_head(fill_fwd([Net(n['safe'].layers)], [(s2c, S), (None, 0), (None, 0)], B), HEAD_SAMPLE, A, e2,
-                      SITE_SAFE_NEXT, a=a2s)], ctr)
-        # launch 2: target constraint critic at (s', a'_safe) and target critics at (s', a')
-        self._run_multi('c.f2' + rk, lambda: [
-            fill_fwd(self._cc_nets('t'), [(s2c, S), (a2s, A), (None, 0)], B, trunk=True),
-            fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (a2, A), (None, 0)], B)], ctr)
+            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)], ctr)
         loss = self._loss_slots(2)
         self._clean_grads(sol.critic_group)
         ch = self.desc.get('c.head')
@@ -684,17 +715,27 @@ class SACEngine:
             noise.randn_like(qshape, used=False)
         ctr = noise.next()
         cc = sol.constraint_critic
-        xa, xs = self.buf('a.x', B, S), self.buf('a.xs', B, S)
+        xa = self.buf('a.x', B, S)   # the actors' shared input save (the wgrad's first-layer Y of both)
         a, lp, u, e = self.buf('a.a', B, A), self.buf('a.lp', B), self.buf('a.u', B, A), self.buf('a.e', B, A)
         a_s, u_s, e_s, am = self.buf('a.as', B, A), self.buf('a.us', B, A), self.buf('a.es', B, A), \
             self.buf('a.am', B, A)
         raw, raws = n['actor'].sy[-1], n['safe'].sy[-1]
         # launch 1: actor and safe actor rsample (saves for backward) + fused heads
-        self._run_multi('a.f1' + noise_tag(e5), lambda: [
-            with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE, A,
-                      e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e),
-            with_head(fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xs), HEAD_RSAMPLE, A,
-                      e6, SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am)], ctr)
+        # (one workgroup runs both policies when their shapes pair: the same input, one
+        # saved copy of it)
+        if pairable(n['actor'], n['safe']):
+            jobs = lambda: [
+                with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
+                                             save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
+                                    e=e),
+                          HEAD_RSAMPLE, A, e6, SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am, second=True)]
+        else:
+            jobs = lambda: [
+                with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE,
+                          A, e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e),
+                with_head(fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A, e6,
+                          SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am)]
+        self._run_multi('a.f1' + noise_tag(e5), jobs, ctr)
         # launch 2: Q_k(s, a), Qc(s, a), Qc(s, a_safe) with saves; Qc(s, tanh(mu_safe)) for lam
         qk = n['q0'] if k == 0 else n['q1']
         self._run_multi(f'a.f2.{k}{int(mlp_mult)}', lambda: [
@@ -757,7 +798,7 @@ class SACEngine:
         sq = self._sq('a', ('a', 's'))
         used = self._run_wgrad('a.wg' + ('f' if sq else ''),
                                lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]], 'a'),
-                                                    (ns, [xs, ns.sy[0], ns.sy[1]], 's')], B, sq))
+                                                    (ns, [xa, ns.sy[0], ns.sy[1]], 's')], B, sq))
         # d alpha_loss / d log_alpha = -exp(log_alpha) * mean(logp + target_entropy) is formed
         # inside the optimizer launch from the alpha-loss sum (src/ssac.py:498-501); under
         # DP the sum is sum-reduced and divided by G*B rows (same value: log_alpha is
@@ -850,11 +891,19 @@ class SACEngine:
         ctr = noise.next()
         a, am = self.buf('m.a', B, A), self.buf('m.am', B, A)
         # launch 1: a ~ pi(s) (rsample) and tanh(mu_safe(s)) via fused heads
-        self._run_multi('m.f1' + noise_tag(e7), lambda: [
-            with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A,
-                      e7, SITE_PI_MULT, a=a),
-            with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A, None,
-                      0, amean=am)], ctr)
+        if pairable(n['actor'], n['safe']):
+            jobs = lambda: [
+                with_head(with_head(fill_fwd([Net(n['actor'].layers), Net(n['safe'].layers)],
+                                             [(self.bs, S), (None, 0), (None, 0)], B, pair=True),
+                                    HEAD_RSAMPLE, A, e7, SITE_PI_MULT, a=a),
+                          HEAD_MEAN, A, None, 0, amean=am, second=True)]
+        else:
+            jobs = lambda: [
+                with_head(fill_fwd([Net(n['actor'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE,
+                          A, e7, SITE_PI_MULT, a=a),
+                with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A,
+                          None, 0, amean=am)]
+        self._run_multi('m.f1' + noise_tag(e7), jobs, ctr)
         # launch 2: constraint critic at (s, a) and at (s, tanh(mu_safe))
         aqc, sqc = self.buf('m.aqc', B), self.buf('m.sqc', B)
         self._run_multi('m.f2', lambda: [

@@ -170,6 +170,17 @@ typedef struct {
                           src/ssac.py:474-494,536-560); NULL: none */
   int ccb_dist;
   float ccb_ratio, ccb_lmin, ccb_lmax;
+  /* multi-job launches: */
+  int pair;            /* non-trunk job, 2 nets of ONE shape on the same input (the twin critics; the
+                          actor and the safe actor): ONE workgroup runs both as paired layers (one
+                          staging, one k-loop per layer pair) instead of one workgroup per net */
+  drpo_policy_head_t head2;   /* pair jobs: the fused head of net[1] (head: net[0]'s) */
+  drpo_mlp_net_t pre;  /* chain (pre.nl > 0): a policy net run first, in the same workgroup, on the
+                          src[0] columns; its head (pre_head, mode 1 or 2) samples the action that
+                          is this job's src[1] column block (cols[1] == A) straight from LDS: the
+                          next-state policy feeding the target critics / certificate
+                          (src/ssac.py:284-294,387-400) without a launch or an HBM round trip */
+  drpo_policy_head_t pre_head;
 } drpo_mlp_fwd_t;
 
 typedef struct {
