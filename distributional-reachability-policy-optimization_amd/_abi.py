@@ -210,6 +210,8 @@ PROTOTYPES.update({
     'drpo_mlp_backward': (c_int, [POINTER(MlpBwd), P]),
     'drpo_mlp_backward_ens': (c_int, [POINTER(MlpBwd), POINTER(EnsUpstream), POINTER(EnsReduce), POINTER(EnsReduce),
                                       P]),
+    'drpo_ens_fit_fb': (c_int, [POINTER(MlpFwd), POINTER(MlpBwd), POINTER(EnsUpstream), POINTER(EnsReduce),
+                                POINTER(EnsReduce), P]),
     'drpo_mlp_wgrad_workspace_size': (c_size_t, [POINTER(WgradItem), c_int]),
     'drpo_mlp_wgrad_tiles': (c_int, [POINTER(WgradItem)]),
     'drpo_mlp_wgrad': (c_int, [POINTER(WgradItem), c_int, P, c_size_t, P]),

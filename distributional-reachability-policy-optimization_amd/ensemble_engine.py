@@ -63,6 +63,27 @@ def ens_fused_shapes(nets, S1):
     return all(din <= 256 and dout <= 256 for (_, _, din, dout, _, _) in nets[0].layers)
 
 
+def ens_fb_shapes(nets, S, A):
+    """The shapes drpo_ens_fit_fb takes (csrc/fit.hip: the fit step's forward, NLL and
+    backward-data in one launch): trunk [S+A <= 64 -> H -> H], heads [H -> H -> S+1 <= 16],
+    swish hidden layers, identity outputs, H = 200 | 256 (the reference default:
+    src/dynamics.py:59-61,85-86, hidden_dim=200, trunk_layers=2, head_hidden_layers=1).
+    DRPO_FIT_FB=0 keeps the two launches (A/B)."""
+    if os.environ.get('DRPO_FIT_FB', '1') == '0' or len(nets) != 3 or S + A > 64 or S + 1 > 16:
+        return False
+    sw = ACT_ID['swish']
+    t = nets[0].layers
+    if len(t) != 2:
+        return False
+    H = t[1][3]
+    if H not in (200, 256) or t[0][3] != H or t[0][4] != sw or t[1][4] != sw:
+        return False
+    for h in (nets[1].layers, nets[2].layers):
+        if len(h) != 2 or h[0][2] != H or h[0][3] != H or h[0][4] != sw or h[1][3] != S + 1 or h[1][4] != 0:
+            return False
+    return True
+
+
 def split_heads_bwd(n, Z):
     if os.environ.get('DRPO_SPLIT_BWD', '1') == '0':     # A/B knob: the paired backward
         return False
@@ -398,6 +419,10 @@ class EnsembleEngine:
         # head_hidden_layers=1, 200-wide); other shapes keep the separate loss launch.
         fused = ens_fused_shapes(nets, S1)
         bd.upstream = 3 if fused else 0   # DRPO_UPSTREAM_ENS
+        # the reference default shapes at split-heads grids: forward + NLL + backward-data
+        # as ONE launch per (row tile, head) (drpo_ens_fit_fb)
+        fb = fused and bool(bd.split_heads) and ens_fb_shapes(nets, S, A)
+        self.fit_fb = fb
         up = EnsUpstream()
         up.D, up.LVR = nets[1].sy[-1].data_ptr(), nets[2].sy[-1].data_ptr()
         up.s_zstride, up.t_zstride, up.b, up.S, up.Z = b * S, b * S1, b, S, Z
@@ -477,10 +502,14 @@ class EnsembleEngine:
             fd.src[0], fd.src[1] = cs.data_ptr() + 4 * k * rows * S, ca.data_ptr() + 4 * k * rows * A
             up.s, up.t = fd.src[0], ct.data_ptr() + 4 * k * rows * S1
             red_in.loss = loss_base + 4 * i
-            _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
+            if not fb:
+                _lib.check(L.drpo_mlp_forward(ctypes.byref(fd), stream), 'ensemble forward')
             if fuse_sh and pending:           # the previous step's bounds are stepped
                 _lib.check(L.drpo_stream_wait_event(main_s, ev_done), 'stream_wait_event')
-            if fused:
+            if fb:
+                _lib.check(L.drpo_ens_fit_fb(ctypes.byref(fd), ctypes.byref(bd), ctypes.byref(up),
+                                             ctypes.byref(red_in), ctypes.byref(red), stream), 'ensemble fit fwd+bwd')
+            elif fused:
                 _lib.check(L.drpo_mlp_backward_ens(ctypes.byref(bd), ctypes.byref(up), ctypes.byref(red_in),
                                                    ctypes.byref(red), stream), 'ensemble backward')
             else:

@@ -345,6 +345,17 @@ int drpo_mlp_backward_multi_actor(const drpo_mlp_bwd_t* jobs_host, const drpo_ml
 int drpo_mlp_backward_ens(const drpo_mlp_bwd_t* desc /* host */, const drpo_ens_upstream_t* up /* host */,
                           const drpo_ens_reduce_t* red_in /* host */, drpo_ens_reduce_t* reduce_out,
                           drpo_stream_t stream);
+/* The model fit step's forward + NLL + backward-data in ONE launch (csrc/fit.hip;
+ * BatchedGaussianEnsemble.fit's compute_loss + loss.backward(), src/dynamics.py:112-122,
+ * 136-153,236-253): replaces drpo_mlp_forward(fwd) + drpo_mlp_backward_ens(bwd, up) for
+ * the ensemble trunk [S+A <= 64 -> H -> H] with diff / log-var heads [H -> H -> S+1 <= 16]
+ * (swish hidden layers, H = 200 | 256). fwd: the split-heads forward descriptor with its
+ * y saves (head output saves and z saves are not written); bwd: the split-heads backward
+ * descriptor (trunk dz + dz2); up: as for drpo_mlp_backward_ens (D / LVR unused). Writes
+ * the same saves, dZ and loss partials as the two launches. */
+int drpo_ens_fit_fb(const drpo_mlp_fwd_t* fwd /* host */, const drpo_mlp_bwd_t* bwd /* host */,
+                    const drpo_ens_upstream_t* up /* host */, const drpo_ens_reduce_t* red_in /* host */,
+                    drpo_ens_reduce_t* reduce_out, drpo_stream_t stream);
 /* Weight gradients of up to 16 layers (items) in ONE launch: gW += dZ^T Y, gb +=
  * colsum(dZ) (the autograd of nn.Linear / BatchedLinear, src/dynamics.py:26-52,
  * src/torch_util.py:190-211), split into (output tile x row chunk) workgroups whose

@@ -27,8 +27,31 @@ def main():
     torch.cuda.synchronize()
     n = 1 << 16
     buf = np.zeros((n, 16), np.uint64)
+    L.drpo_debug_stamps_wgrad_clear()
+    torch.cuda.synchronize()
     m.fit(alg.replay_buffer, steps=1)
     torch.cuda.synchronize()
+    if m.engine.fit_fb:     # the one-launch step (csrc/fit.hip FSTAMP 0..8)
+        L.drpo_debug_stamps_fit.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        fb = np.zeros((4096, 16), np.uint64)
+        L.drpo_debug_stamps_fit(fb.ctypes.data, 4096)
+        fb = fb.astype(np.int64)
+        fb = fb[fb[:, 0] > 0]
+        print(f'== fit_fb_kernel (forward + NLL + backward-data): {len(fb)} workgroups')
+        for a, b, name in ((0, 1, 'stage x'), (1, 2, 'trunk L1'), (2, 3, 'trunk L2'), (3, 4, 'heads hidden+out'),
+                           (4, 5, 'NLL'), (5, 6, 'B1 head out^T'), (6, 7, 'B2 head hidden^T'), (7, 8, 'B3 trunk L2^T'),
+                           (0, 9, ' preloads'), (9, 1, ' staging'), (1, 10, ' L1 mma'), (10, 11, ' L1 next prefetch'),
+                           (11, 12, ' L1 epilogue'), (12, 2, ' L1 barrier'), (5, 13, ' B1 mma'),
+                           (13, 14, ' B1 next prefetch'), (14, 15, ' B1 epilogue'), (15, 6, ' B1 barrier')):
+            if fb[:, b].max() == 0 or fb[:, a].max() == 0:
+                continue
+            d = fb[:, b] - fb[:, a]
+            print(f'   {name:20s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
+        d = fb[:, 8] - fb[:, 0]
+        print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
+        t0 = fb[:, 0].min()
+        wgrad_phases(L)
+        return
     L.drpo_debug_stamps(buf.ctypes.data, n)
     # forward (mlp_fwd_kernel STAMP rows 0..: 0 start, 1 input staged, 2/3 trunk layers,
     # 6/7 head 1 layers (lb.y == 0), 10/11 head 2 layers (lb.y == 1))
@@ -63,6 +86,23 @@ def main():
     if ok.any():
         d = bw[ok, 12] - bw[ok, 0]
         print(f'   workgroup total       mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f} cyc')
+
+def wgrad_phases(L):
+    """the step's weight-gradient + Adam launch (csrc/wgrad.hip STAMPG 0..5)"""
+    L.drpo_debug_stamps_wgrad.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    st = np.zeros((1 << 14, 8), np.uint64)
+    L.drpo_debug_stamps_wgrad(st.ctypes.data, 1 << 14)
+    st = st.astype(np.int64)
+    st = st[st[:, 0] > 0]
+    print(f'== mlp_wgrad_kernel (+ Adam): {len(st)} workgroups')
+    for a, b, name in ((0, 5, 'ring fill'), (0, 1, 'main loop'), (1, 2, 'lds reduce'), (2, 3, 'slab + ticket'),
+                       (3, 4, 'last finish'), (2, 4, 'finish (adam)'), (0, 4, 'total')):
+        ok = (st[:, a] > 0) & (st[:, b] > 0)
+        if ok.any():
+            d = st[ok, b] - st[ok, a]
+            print(f'   {name:20s} mean {d.mean():8.0f} min {d.min():8.0f} p90 {np.percentile(d, 90):8.0f} '
+                  f'max {d.max():8.0f} cyc  (n={ok.sum()})')
+
 
 if __name__ == '__main__':
     main()

@@ -461,3 +461,56 @@ def test_fit_fused_adam_matches_separate_step(c):
     assert int((o_f[5] != 0).sum()) == 0           # the gradient is left zeroed
     np.testing.assert_allclose(l_p, l_f, rtol=1e-5)
     _close(o_p[0], o_f[0].cpu().numpy(), 2e-5, 'paired vs split backward: parameters')
+
+
+@pytest.mark.parametrize('c', [1, 2, 3])
+def test_fit_fb_matches_two_launches(c):
+    """The fit step's forward + NLL + backward-data as ONE launch (drpo_ens_fit_fb,
+    csrc/fit.hip) against the split-heads forward + drpo_mlp_backward_ens it replaces:
+    the same saves (x, trunk y's, heads' hidden y's), every dZ the weight gradients read
+    (trunk dz + dz2, both heads) and the step losses, from the same start and minibatch
+    (one step, production noise). The trunk and hidden layers take the same MFMA order
+    (bitwise); the heads' output layers are reduced split-K over the 4 waves that own the
+    hidden columns instead of the separate forward's order, so D / log-var and everything
+    downstream differ by summation order only: rtol 2e-5 on the saves, 1e-4 of each
+    tensor's max-abs on the dZ."""
+    import os
+    from drpo_amd.rng import DeviceNoise
+    alg, cd = _alg(c, B=256)
+    m = alg.model_ensemble
+    eng = m.engine
+    _fill(alg, cd['env'], 30000, 8)
+    g = m.group
+    m.optimizer._ensure_state()
+    start = [g.data.clone(), m.optimizer.m.clone(), m.optimizer.v.clone(), m.optimizer.step_count]
+    names = ['fit.x', 'fit.sy00', 'fit.sy01', 'fit.sy10', 'fit.sy20'] + \
+        [f'fit.dz{j}{l}' for j in range(3) for l in range(2)] + ['fit.dzb0', 'fit.dzb1']
+
+    def run(fb):
+        g.data.copy_(start[0])
+        m.optimizer.m.copy_(start[1])
+        m.optimizer.v.copy_(start[2])
+        m.optimizer.step_count = start[3]
+        g.mark_dirty()
+        g.ensure_packed()
+        os.environ['DRPO_FIT_FB'] = '1' if fb else '0'
+        eng.ws.clear()
+        eng.wg_ws.clear()
+        losses = m.fit(alg.replay_buffer, steps=1, noise=DeviceNoise(4321))
+        torch.cuda.synchronize()
+        assert eng.fit_fb == fb and eng.fit_path == 'fused'
+        return losses, {k: eng.ws[k].clone() for k in names}
+
+    try:
+        l_f, o_f = run(True)
+        l_s, o_s = run(False)
+    finally:
+        os.environ.pop('DRPO_FIT_FB', None)
+    np.testing.assert_allclose(l_f, l_s, rtol=2e-5)
+    for k in names:
+        a, b = o_f[k].cpu().numpy(), o_s[k].cpu().numpy()
+        assert np.isfinite(a).all(), k
+        if k.startswith('fit.dz'):
+            np.testing.assert_allclose(a, b, rtol=0, atol=1e-4 * float(np.abs(b).max()) + 1e-30, err_msg=k)
+        else:
+            np.testing.assert_allclose(a, b, rtol=2e-5, atol=1e-6, err_msg=k)
