@@ -477,8 +477,15 @@ __global__ __launch_bounds__(FF_NT) void fit_fb_kernel(FitFbArgs args) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   FitK& k = *(FitK*)__builtin_amdgcn_kernarg_segment_ptr();
   (void)args;
-  if (k.f.net[0].L[1].dout == 200) fit_fb_body<13>(k, smem);
-  else fit_fb_body<16>(k, smem);
+#ifndef DRPO_FIT_REPS
+#define DRPO_FIT_REPS 1   // probe builds only: the body run R times (its last run's stamps kept)
+#endif
+#pragma nounroll
+  for (int rep = 0; rep < DRPO_FIT_REPS; ++rep) {
+    if (k.f.net[0].L[1].dout == 200) fit_fb_body<13>(k, smem);
+    else fit_fb_body<16>(k, smem);
+    if (DRPO_FIT_REPS > 1) __syncthreads();
+  }
 }
 
 static_assert(sizeof(FitFbArgs) <= 4096, "fused fit kernarg");

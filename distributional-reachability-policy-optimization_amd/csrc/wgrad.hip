@@ -96,6 +96,7 @@ struct WgradPlan {
   int z2;                  // a second dZ term (item dz2)
   int pk_layer;            // fused Adam: the item's matrix in the pack map (-1: none)
   int pk_z0;               // its first member within that matrix (a member shard's slice)
+  int vf;                  // 64x64 tiles, 16-byte aligned rows: the finish in float4s
   int64_t first_unit;      // first logical workgroup of the item
   int64_t first_tile;      // first arrival counter of the item
   int64_t slab_off;        // first slab float of the item (tiles with nch > 1)
@@ -328,12 +329,29 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
     }
   }
   __syncthreads();
-  // thread t owns tile elements t + 256 e: il = t % TI, ol = t / TI + (256 / TI) e
+  // Thread t owns tile elements t + 256 e: il = t % TI, ol = t / TI + (256 / TI) e; with
+  // P.vf (64x64 tiles) it owns 4 runs of 4 consecutive inputs instead: run f = t + 256 j
+  // is row ol = f / 16, inputs 4 (f % 16) .. + 3 -- the gradient / Adam reads and writes
+  // then go as float4s (a quarter of the memory instructions; the forward mirror's 4
+  // components are one float4 too). A slab (nch > 1) stores element e at t + 256 e in
+  // either mapping: the writer and the last arriver of a tile use the same one.
+  const bool vf = TO == 64 && TI == 64 && P.vf;
+  auto elem = [&](int e, int& ol, int& il) {
+    if (vf) {
+      const int f = tid + WG_NT * (e >> 2);
+      ol = f >> 4;
+      il = ((f & 15) << 2) + (e & 3);
+    } else {
+      const int idx = tid + WG_NT * e;
+      ol = idx / TI;
+      il = idx % TI;
+    }
+  };
   float pv[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const int idx = tid + WG_NT * e;
-    const int ol = idx / TI, il = idx % TI;
+    int ol, il;
+    elem(e, ol, il);
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < WG_NW; ++w) s += R[slab_index<TO, TI>(w, ol, il)];
@@ -359,18 +377,41 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
   const bool adam = a.has_adam;
   const int64_t eW = adam ? gW - a.adam.g : 0, eb = adam ? gb - a.adam.g : 0;   // flat element offsets
   float ap[E], am[E], av[E], bp = 0.f, bm = 0.f, bvv = 0.f;
-  auto load_grad = [&]() {
+  auto ld4 = [&](const float* base, int64_t k, bool in, float* dst) {
+    const f32x4 v = in ? *reinterpret_cast<const f32x4*>(base + k) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int idx = tid + WG_NT * e;
-      const int o = o0 + idx / TI, i = i0 + idx % TI;
-      const bool in = o < dout && i < din;
-      const int64_t k = (int64_t)o * din + i;
-      gv[e] = in ? gW[k] : 0.f;
-      if (adam) {
-        ap[e] = in ? a.adam.p[eW + k] : 0.f;
-        am[e] = in ? a.adam.m[eW + k] : 0.f;
-        av[e] = in ? a.adam.v[eW + k] : 0.f;
+    for (int c = 0; c < 4; ++c) dst[c] = v[c];
+  };
+  auto load_grad = [&]() {
+    if (vf) {   // din % 4 == 0: a run of 4 is wholly inside or outside the matrix
+#pragma unroll
+      for (int j = 0; j < E / 4; ++j) {
+        int ol, il;
+        elem(4 * j, ol, il);
+        const int o = o0 + ol, i = i0 + il;
+        const bool in = o < dout && i < din;
+        const int64_t k = (int64_t)o * din + i;
+        ld4(gW, k, in, gv + 4 * j);
+        if (adam) {
+          ld4(a.adam.p + eW, k, in, ap + 4 * j);
+          ld4(a.adam.m + eW, k, in, am + 4 * j);
+          ld4(a.adam.v + eW, k, in, av + 4 * j);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        int ol, il;
+        elem(e, ol, il);
+        const int o = o0 + ol, i = i0 + il;
+        const bool in = o < dout && i < din;
+        const int64_t k = (int64_t)o * din + i;
+        gv[e] = in ? gW[k] : 0.f;
+        if (adam) {
+          ap[e] = in ? a.adam.p[eW + k] : 0.f;
+          am[e] = in ? a.adam.m[eW + k] : 0.f;
+          av[e] = in ? a.adam.v[eW + k] : 0.f;
+        }
       }
     }
     gbv = bias_mine ? gb[o0 + tid] : 0.f;
@@ -439,10 +480,44 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
     const int64_t mb = md ? md->poff[P.pk_layer] + (int64_t)(P.pk_z0 + zb) * ncb * nks * 256 : 0;
     float* PM = md ? md->P : nullptr;
     float* PTM = md ? md->PT : nullptr;
+    if (vf) {
+#pragma unroll
+      for (int j = 0; j < E / 4; ++j) {
+        int ol, il;
+        elem(4 * j, ol, il);
+        const int o = o0 + ol, i = i0 + il;
+        if (o >= dout || i >= din) continue;
+        const int64_t k = (int64_t)o * din + i;
+        f32x4 p4, m4, v4;
+        bool nz = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float pe = ap[4 * j + c], me = am[4 * j + c], ve = av[4 * j + c];
+          adam_step(a.adam, 1.f, gv[4 * j + c] + pv[4 * j + c], pe, me, ve);
+          p4[c] = pe;
+          m4[c] = me;
+          v4[c] = ve;
+          nz = nz || gv[4 * j + c] != 0.f;
+        }
+        *reinterpret_cast<f32x4*>(a.adam.p + eW + k) = p4;
+        *reinterpret_cast<f32x4*>(a.adam.m + eW + k) = m4;
+        *reinterpret_cast<f32x4*>(a.adam.v + eW + k) = v4;
+        if (nz) *reinterpret_cast<f32x4*>(gW + k) = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (PM)   // i .. i+3 are the 4 components of one lane of fragment (o>>4, i>>4)
+          *reinterpret_cast<f32x4*>(PM + mb + ((int64_t)((o >> 4) * nks + (i >> 4)) << 8) +
+                                    ((((i >> 2) & 3) * 16 + (o & 15)) << 2)) = p4;
+        if (PTM)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            PTM[mb + ((int64_t)((i >> 4) * ncb + (o >> 4)) << 8) + (((((o >> 2) & 3) * 16 + ((i + c) & 15))) << 2) +
+                (o & 3)] = p4[c];
+      }
+    } else
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int idx = tid + WG_NT * e;
-      const int o = o0 + idx / TI, i = i0 + idx % TI;
+      int ol, il;
+      elem(e, ol, il);
+      const int o = o0 + ol, i = i0 + il;
       if (o < dout && i < din) {
         const int64_t k = (int64_t)o * din + i;
         float pe = ap[e], me = am[e], ve = av[e];
@@ -469,10 +544,27 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
   }
   // gradient += sum (the caller's gradient is zeroed or holds terms to accumulate)
   float sq = 0.f;
+  if (vf) {
+#pragma unroll
+    for (int j = 0; j < E / 4; ++j) {
+      int ol, il;
+      elem(4 * j, ol, il);
+      const int o = o0 + ol, i = i0 + il;
+      if (o >= dout || i >= din) continue;
+      f32x4 v4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        v4[c] = gv[4 * j + c] + pv[4 * j + c];
+        sq = fmaf(v4[c], v4[c], sq);
+      }
+      *reinterpret_cast<f32x4*>(gW + (size_t)o * din + i) = v4;
+    }
+  } else
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const int idx = tid + WG_NT * e;
-    const int o = o0 + idx / TI, i = i0 + idx % TI;
+    int ol, il;
+    elem(e, ol, il);
+    const int o = o0 + ol, i = i0 + il;
     if (o < dout && i < din) {
       const float v = gv[e] + pv[e];
       gW[(size_t)o * din + i] = v;
@@ -589,6 +681,10 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     ++m;
   }
   a.n = m;
+  static const bool vf_env = [] {   // A/B knob: the float4 finish (WgradPlan.vf)
+    const char* e = getenv("DRPO_WGRAD_VF");
+    return !(e && e[0] == '0');
+  }();
   // chunk sizes: every unit about the same cost, all units resident at once (<= 2 per CU)
   static const int per_cu = [] {   // A/B knob (profiles/wgrad_probe.py)
     const char* e = getenv("DRPO_WGRAD_PER_CU");
@@ -635,6 +731,8 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     P.va = (I.dout & 3) == 0 && ((uintptr_t)I.dz & 15) == 0 && ((uintptr_t)I.dz2 & 15) == 0 && (I.zstride & 3) == 0;
     P.z2 = I.dz2 != nullptr;
     P.vb = (I.din & 3) == 0 && ((uintptr_t)I.y & 15) == 0 && (I.ystride & 3) == 0;
+    P.vf = s.to == 64 && s.ti == 64 && (I.din & 3) == 0 && ((uintptr_t)I.gW & 15) == 0 && (I.gwstride & 3) == 0 &&
+           vf_env;
     P.first_unit = unit;
     P.first_tile = tile;
     P.slab_off = slab;
@@ -745,6 +843,11 @@ static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_re
       }
       DRPO_REQUIRE(p.a.pl[k].pk_layer >= 0, "drpo_mlp_wgrad_adam: item %d is not a matrix of the pack map", k);
     }
+    // the float4 finish also reads / writes p, m, v at the gradient's flat offsets
+    const bool al = ((uintptr_t)adam->p & 15) == 0 && ((uintptr_t)adam->m & 15) == 0 &&
+                    ((uintptr_t)adam->v & 15) == 0 && ((uintptr_t)adam->g & 15) == 0 &&
+                    (!mh || (((uintptr_t)mh->P & 15) == 0 && ((uintptr_t)mh->PT & 15) == 0));
+    for (int k = 0; k < p.a.n; ++k) p.a.pl[k].vf = p.a.pl[k].vf && al && ((p.a.it[k].gW - adam->g) & 3) == 0;
   }
   const int64_t blocks = p.a.units + (red ? 1 : 0) + (nsums ? 1 : 0);
   if (blocks == 0) return DRPO_OK;
