@@ -55,6 +55,12 @@ constexpr int WG_NT = WG_NW * 64;
 #define DRPO_WG_D 3
 #endif
 constexpr int WG_D = DRPO_WG_D;          // register ring slots (k-groups of 4 rows each; A/B macro)
+#ifndef DRPO_WGRAD_EARLY
+#define DRPO_WGRAD_EARLY 1               // A/B macro: single-chunk tiles load their finish operands early
+#endif
+#ifndef DRPO_WGRAD_PTT
+#define DRPO_WGRAD_PTT 1                 // A/B macro: the float4 finish's transposed refresh through LDS
+#endif
 #ifndef DRPO_WGRAD_ACQREL
 #define DRPO_WGRAD_ACQREL 0              // A/B macro: acq_rel ticket (see the memory-model note)
 #endif
@@ -301,34 +307,6 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
   }
 
   STAMPG(1);
-  // the 4 waves' partial tiles -> LDS slabs (conflict-free: lanes write consecutive words)
-  float* R = lds;
-#pragma unroll
-  for (int m = 0; m < MA; ++m)
-#pragma unroll
-    for (int n = 0; n < MB; ++n)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) R[(wave * NA + m * MB + n) * WG_SLD + rr * 64 + lane] = acc[m][n][rr];
-  // bias partials: sum over the 4 row lanes g of each column, then over waves (LDS)
-  float* Rb = lds + WG_NW * NA * WG_SLD;      // [WG_NW][TO]
-  if (do_bias) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float s = bsum[c];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      bsum[c] = s;
-    }
-    if (g == 0) {
-      if constexpr (WA == 4) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) Rb[wave * TO + 4 * l15 + c] = bsum[c];
-      } else {
-        Rb[wave * TO + l15] = bsum[0];
-      }
-    }
-  }
-  __syncthreads();
   // Thread t owns tile elements t + 256 e: il = t % TI, ol = t / TI + (256 / TI) e; with
   // P.vf (64x64 tiles) it owns 4 runs of 4 consecutive inputs instead: run f = t + 256 j
   // is row ol = f / 16, inputs 4 (f % 16) .. + 3 -- the gradient / Adam reads and writes
@@ -347,28 +325,14 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
       il = idx % TI;
     }
   };
-  float pv[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    int ol, il;
-    elem(e, ol, il);
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < WG_NW; ++w) s += R[slab_index<TO, TI>(w, ol, il)];
-    pv[e] = s;
-  }
-  float pb = 0.f;
-  if (do_bias && tid < TO) {
-#pragma unroll
-    for (int w = 0; w < WG_NW; ++w) pb += Rb[w * TO + tid];
-  }
-  STAMPG(2);
   constexpr int SL = TO * TI + TO;            // slab floats per unit (tile + bias)
   float* gW = I.gW + (size_t)zb * I.gwstride;
   float* gb = I.gb + (size_t)zb * I.gbstride;
   float* red = lds + WG_NW * NA * WG_SLD + WG_NW * TO;   // 4 floats
   // the gradient's current values: loaded by the workgroup that finishes the tile,
-  // before (and in flight with) the slab loads; every load precedes the first store
+  // before (and in flight with) the slab loads; every load precedes the first store.
+  // A single-chunk tile (nch == 1) is finished by its only workgroup: its loads are
+  // issued here, ahead of the partial tiles' LDS reduction, which covers their latency
   float gv[E];
   const bool bias_mine = do_bias && tid < TO && o0 + tid < dout;
   float gbv = 0.f;
@@ -421,6 +385,51 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
       bvv = a.adam.v[eb + o0 + tid];
     }
   };
+  if (DRPO_WGRAD_EARLY && P.nch == 1) load_grad();
+  // the 4 waves' partial tiles -> LDS slabs (conflict-free: lanes write consecutive words)
+  float* R = lds;
+#pragma unroll
+  for (int m = 0; m < MA; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) R[(wave * NA + m * MB + n) * WG_SLD + rr * 64 + lane] = acc[m][n][rr];
+  // bias partials: sum over the 4 row lanes g of each column, then over waves (LDS)
+  float* Rb = lds + WG_NW * NA * WG_SLD;      // [WG_NW][TO]
+  if (do_bias) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float s = bsum[c];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      bsum[c] = s;
+    }
+    if (g == 0) {
+      if constexpr (WA == 4) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) Rb[wave * TO + 4 * l15 + c] = bsum[c];
+      } else {
+        Rb[wave * TO + l15] = bsum[0];
+      }
+    }
+  }
+  __syncthreads();
+  float pv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    int ol, il;
+    elem(e, ol, il);
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WG_NW; ++w) s += R[slab_index<TO, TI>(w, ol, il)];
+    pv[e] = s;
+  }
+  float pb = 0.f;
+  if (do_bias && tid < TO) {
+#pragma unroll
+    for (int w = 0; w < WG_NW; ++w) pb += Rb[w * TO + tid];
+  }
+  STAMPG(2);
   if (P.nch > 1) {
     float* my = a.slab + P.slab_off + (tile_local * P.nch + ch) * SL;
 #pragma unroll
@@ -468,7 +477,7 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
         }
       }
     }
-  } else {
+  } else if (!DRPO_WGRAD_EARLY) {
     load_grad();
   }
   if (adam) {
@@ -506,11 +515,41 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
         if (PM)   // i .. i+3 are the 4 components of one lane of fragment (o>>4, i>>4)
           *reinterpret_cast<f32x4*>(PM + mb + ((int64_t)((o >> 4) * nks + (i >> 4)) << 8) +
                                     ((((i >> 2) & 3) * 16 + (o & 15)) << 2)) = p4;
-        if (PTM)
+        if (PTM && !DRPO_WGRAD_PTT)
 #pragma unroll
           for (int c = 0; c < 4; ++c)
             PTM[mb + ((int64_t)((i >> 4) * ncb + (o >> 4)) << 8) + (((((o >> 2) & 3) * 16 + ((i + c) & 15))) << 2) +
                 (o & 3)] = p4[c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ap[4 * j + c] = p4[c];   // the new parameters (the transposed refresh)
+      }
+      if (PTM && DRPO_WGRAD_PTT) {
+        // transposed mirror: a float4 there is 4 consecutive outputs of one input, so the
+        // tile goes through LDS ([64][65] floats over the partial-tile slabs) and each
+        // thread stores 4 such float4s instead of 16 scattered floats
+        float* T = lds;
+        __syncthreads();   // every thread's reads of the partial-tile slabs are done
+#pragma unroll
+        for (int j = 0; j < E / 4; ++j) {
+          int ol, il;
+          elem(4 * j, ol, il);
+          const bool in = o0 + ol < dout && i0 + il < din;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) T[ol * 65 + il + c] = in ? ap[4 * j + c] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < E / 4; ++j) {
+          const int f = tid + WG_NT * j;
+          const int il = f >> 4, ol = (f & 15) << 2;   // input il, outputs ol .. ol + 3
+          const int o = o0 + ol, i = i0 + il;
+          if (o >= dout || i >= din) continue;
+          f32x4 v;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) v[c] = T[(ol + c) * 65 + il];   // zero past dout: the padding
+          *reinterpret_cast<f32x4*>(PTM + mb + ((int64_t)((i >> 4) * ncb + (o >> 4)) << 8) +
+                                    ((((o >> 2) & 3) * 16 + (i & 15)) << 2)) = v;
+        }
       }
     } else
 #pragma unroll
