@@ -291,6 +291,7 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
 #pragma unroll
   for (int v = 0; v < (Z2 ? WG_D : 1); ++v) ra2[v] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int steps = (nj + WG_D - 1 + WG_D - 1) / WG_D * WG_D;
+  STAMPG(6);
   for (int s0 = 0; s0 < steps; s0 += WG_D) {
 #pragma unroll
     for (int v = 0; v < WG_D; ++v) {
@@ -302,7 +303,8 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
         use(s0 + v - (WG_D - 1), ra[(v + 1) % WG_D], rb[(v + 1) % WG_D], ra2[Z2 ? (v + 1) % WG_D : 0]);
     }
 #ifdef DRPO_STAMPS
-    if (s0 == WG_D) STAMPG(5);   // the first k-group consumed: the ring's fill latency
+    if (s0 == 0) STAMPG(7);      // the first k-group consumed: the ring's fill latency
+    if (s0 == WG_D) STAMPG(5);
 #endif
   }
 

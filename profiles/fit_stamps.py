@@ -95,7 +95,7 @@ def wgrad_phases(L):
     st = st.astype(np.int64)
     st = st[st[:, 0] > 0]
     print(f'== mlp_wgrad_kernel (+ Adam): {len(st)} workgroups')
-    for a, b, name in ((0, 5, 'ring fill'), (0, 1, 'main loop'), (1, 2, 'lds reduce'), (2, 3, 'slab + ticket'),
+    for a, b, name in ((0, 6, 'setup'), (6, 7, 'first k-group'), (7, 5, 'next 3 k-groups'), (0, 5, 'ring fill'), (0, 1, 'main loop'), (1, 2, 'lds reduce'), (2, 3, 'slab + ticket'),
                        (3, 4, 'last finish'), (2, 4, 'finish (adam)'), (0, 4, 'total')):
         ok = (st[:, a] > 0) & (st[:, b] > 0)
         if ok.any():

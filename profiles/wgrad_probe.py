@@ -94,7 +94,9 @@ def stamps(items, rows):
         d = st[ok, b] - st[ok, a]
         out[name] = [int(d.mean()), int(d.min()), int(np.percentile(d, 90)), int(d.max()), int(ok.sum())] \
             if ok.any() else None
-    stat(0, 5, 'ring_fill')       # start -> first k-group consumed (units with >= D k-groups)
+    stat(0, 6, 'setup')           # start -> ring loop entry (item lookup, unit decode)
+    stat(6, 7, 'first_kgroup')    # the first k-group's loads -> its MFMAs issued
+    stat(0, 5, 'ring_fill')       # start -> 4th k-group consumed (units with >= D k-groups)
     stat(0, 1, 'main_loop')       # start -> k loop done
     stat(1, 2, 'lds_reduce')
     stat(2, 3, 'slab_ticket')
