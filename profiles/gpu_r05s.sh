@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 5: weight-gradient unit setup -- plan / item fields pinned in one scalar batch
+# (DRPO_WGRAD_KPIN) vs copied unpinned: wgrad tests, fit + SAC wgrad timings, stamps.
+OUT=gpurun_out/${1:-r05s}
+mkdir -p $OUT
+export TMPDIR=/tmp
+LIBD=$PWD/distributional-reachability-policy-optimization_amd
+timeout -k 10 300 python -u -m pytest tests/test_gpu_wgrad.py tests/test_gpu_configs.py -m gpu -x -q --timeout 120 \
+  --timeout-method thread -k "wgrad or fit" > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc $rc" >> $OUT/pytest.log; tail -3 $OUT/pytest.log
+[ $rc -eq 0 ] || exit 1
+for rep in 1 2; do
+  for v in "X=1" "DRPO_LIB_OVERRIDE=$LIBD/libdrpo_hip_nopin.so"; do
+    env $v FIT_STEPS=300 timeout -k 10 120 python -u profiles/fit_profile.py > $OUT/fit.log 2>&1 || exit 1
+    echo "[$v]: $(tail -1 $OUT/fit.log)"
+    env $v timeout -k 10 180 python -u profiles/sac_micro.py --steps 10 > $OUT/sac_micro.json 2> $OUT/sac_micro.err || exit 1
+    python - $OUT/sac_micro.json <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(' '.join(f"{k}:{v['avg_ms']*1e3:.1f}us" for k, v in d.items() if k.startswith('mlp_wgrad') and isinstance(v, dict)))
+PY
+  done
+done
+for t in "" "_nopin"; do
+  DRPO_LIB_OVERRIDE=$LIBD/libdrpo_hip_stamps$t.so timeout -k 10 120 python -u profiles/fit_stamps.py > $OUT/fit_stamps$t.txt 2>&1 || exit 1
+  echo "stamps$t"; grep -v "^/opt" $OUT/fit_stamps$t.txt | tail -9
+done
