@@ -237,12 +237,15 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
   const auto& P = a.pl[q];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, l15 = lane & 15;
-  const int it_i = (int)(u % P.nti);
-  int64_t rest = u / P.nti;
-  const int it_o = (int)(rest % P.nto);
-  rest /= P.nto;
-  const int ch = (int)(rest % P.nch);
-  const int zb = (int)(rest / P.nch);
+  // 32-bit decode (an item has < 2^31 units): a 64-bit division expands to a long
+  // stretch of scalar code, fetched cold by every workgroup at every dispatch
+  const unsigned uu = (unsigned)u;
+  const int it_i = (int)(uu % (unsigned)P.nti);
+  unsigned rest = uu / (unsigned)P.nti;
+  const int it_o = (int)(rest % (unsigned)P.nto);
+  rest /= (unsigned)P.nto;
+  const int ch = (int)(rest % (unsigned)P.nch);
+  const int zb = (int)(rest / (unsigned)P.nch);
   const int64_t tile_local = ((int64_t)zb * P.nto + it_o) * P.nti + it_i;
   const int dout = I.dout, din = I.din;
   const float* __restrict__ dz = I.dz + (size_t)zb * I.zstride;
@@ -663,10 +666,18 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs args) {
   for (int i = 1; i < WG_MAXITEMS; ++i) q += bid >= a.first[i] ? 1 : 0;
   const auto& P = a.pl[q];
   const int64_t u = bid - P.first_unit;
-  if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
-  else if (P.to == 64) wgrad_unit_v<64, 16>(a, q, u, wsm);
-  else if (P.ti == 64) wgrad_unit_v<16, 64>(a, q, u, wsm);
-  else wgrad_unit_v<16, 16>(a, q, u, wsm);
+#ifndef DRPO_WGRAD_REPS
+#define DRPO_WGRAD_REPS 1   // timing probes only: the unit run R times (results then wrong)
+#endif
+#pragma nounroll
+  for (int rep = 0; rep < DRPO_WGRAD_REPS; ++rep) {
+    if (DRPO_WGRAD_REPS > 1) STAMPG(0);
+    if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
+    else if (P.to == 64) wgrad_unit_v<64, 16>(a, q, u, wsm);
+    else if (P.ti == 64) wgrad_unit_v<16, 64>(a, q, u, wsm);
+    else wgrad_unit_v<16, 16>(a, q, u, wsm);
+    if (DRPO_WGRAD_REPS > 1) __syncthreads();
+  }
 }
 
 static_assert(sizeof(WgradArgs) <= 4096, "weight-gradient kernarg");
