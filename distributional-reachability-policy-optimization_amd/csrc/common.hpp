@@ -327,6 +327,9 @@ __device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N,
 // 16-float-stride partial slabs) costs a lane select per store and measured SLOWER on
 // one box, alternating (profiles/r05/swz_ab: rollout frac 0.434-0.435 vs 0.466, SAC 63.5
 // vs 65.7 TFLOP/s, fit 0.0757 vs 0.0735 ms). Kept as an A/B macro, off.
+#ifndef DRPO_PROBE_NOSAVE
+#define DRPO_PROBE_NOSAVE 0   // timing probes only: the MLP epilogues skip their global saves (results wrong)
+#endif
 #ifndef DRPO_LDS_SWZ
 #define DRPO_LDS_SWZ 0   // A/B macro, measured slower (profiles/r05/swz_ab): off
 #endif
@@ -335,6 +338,29 @@ __device__ __forceinline__ int swz_row(int r, int g) { return DRPO_LDS_SWZ ? r ^
 template <int X>
 __device__ __forceinline__ float swz_pick(const f32x4& v, int r, int g) {
   return (DRPO_LDS_SWZ && (g & 1)) ? v[r ^ X] : v[r];
+}
+
+// A layer's [rows][N] output tile saved to global from LDS after the layer's barrier,
+// as 16-byte stores by every thread of the workgroup (at N = 256 one wave-instruction
+// writes one whole 1 KB row) instead of the epilogue's row-strided 4-byte stores (four
+// 64 B pieces per wave-instruction, 4x the store instructions): DRPO_DEFER_SAVES.
+// N % 4 == 0 and a 16-byte aligned destination (checked by the callers); rows < nrows.
+#ifndef DRPO_DEFER_SAVES
+#define DRPO_DEFER_SAVES 1   // A/B macro
+#endif
+template <int NT, int ROWS>
+__device__ __forceinline__ void save_tile_lds(const float* t, int ldt, float* gy, int N, int nrows) {
+  const int n4 = N >> 2;
+  for (int e = threadIdx.x; e < ROWS * n4; e += NT) {
+    const int r = n4 == 64 ? e >> 6 : e / n4, c = e - r * n4;
+    if (r < nrows)
+      gstore(reinterpret_cast<f32x4*>(gy + (size_t)r * N) + c, *reinterpret_cast<const f32x4*>(t + r * ldt + 4 * c));
+  }
+}
+
+// a layer save the caller may defer to save_tile_lds: post-activation only, 4-aligned width
+__device__ __forceinline__ bool save_deferrable(const float* gy, const float* gz, int N) {
+  return DRPO_DEFER_SAVES && gy && !gz && N > 16 && (N & 3) == 0 && (((uintptr_t)gy) & 15) == 0;
 }
 
 template <int NW, int RB, int MAXC, int ACT>
@@ -358,8 +384,8 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
         if (col < N && row < gs.nrows) {
-          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+          if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -768,8 +794,8 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
     const int row = rb * 16 + rr;
     if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
     if (col < N && row < gs.nrows) {
-      if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-      if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+      if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+      if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
     }
   }
 }
@@ -860,8 +886,8 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
         const float y = act_fn<ACT>(z);
         out[row * ldo + col] = (col < nn) ? y : 0.f;
         if (col < nn && row < gs.nrows) {
-          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+          if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -980,8 +1006,8 @@ __device__ __forceinline__ void tile_dense_pair2_core(const float* in1, const fl
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < nn) ? y : 0.f;
         if (col < nn && row < gs.nrows) {
-          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+          if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -1210,8 +1236,8 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
     out[row * ldo + col] = (col < nn) ? y : 0.f;
     const GSave& gs = which ? gs2 : gs1;
     if (col < nn && row < gs.nrows) {
-      if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-      if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+      if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+      if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
     }
   }
 }

@@ -82,6 +82,15 @@ DRPO_API int drpo_debug_stamps_clear() {
   do {            \
   } while (0)
 #endif
+#ifndef DRPO_DEFER_NET
+#define DRPO_DEFER_NET 1    // deferred saves (save_tile_lds) in run_net_g / heads_pair / pair_nets
+#endif
+#ifndef DRPO_DEFER_HEADS
+#define DRPO_DEFER_HEADS 0   // on: 60 VGPRs spilled in mlp_fwd_multi_kernel<1> (the paired heads layer)
+#endif
+#ifndef DRPO_DEFER_PAIR
+#define DRPO_DEFER_PAIR 0   // on: the paired nets (a.f1) 2 us slower (profiles/r05/defer_saves)
+#endif
 template <int ACT, int RB>
 __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const drpo_mlp_layer_t& L, const float* W,
                                               const float* b, float* out, int ldo, float* red, const GSave& gs) {
@@ -237,8 +246,12 @@ __device__ __forceinline__ float* run_net_g(const drpo_mlp_net_t& __restrict__ n
   const int nl = n.nl;
   for (int l = 0; l < nl; ++l) {
     float* out = (cur == bufA) ? bufB : bufA;
-    run_layer<RB>(cur, LDH, n.L[l], z, rows, row0, nrows, out, red);
+    const drpo_mlp_layer_t& L = n.L[l];
+    const GSave gs = layer_save(L, z, rows, row0, nrows);
+    const bool defer = DRPO_DEFER_NET && save_deferrable(gs.gy, gs.gz, L.dout);
+    run_layer<RB>(cur, LDH, L, z, rows, row0, nrows, out, red, !defer);
     lds_barrier();
+    if (defer) save_tile_lds<FW_NT, 16 * RB>(out, LDH, gs.gy, L.dout, nrows);
     STAMP(2 + l);
     cur = out;
   }
@@ -266,11 +279,18 @@ __device__ __forceinline__ void heads_pair_act(const drpo_mlp_fwd_t* __restrict_
   const drpo_mlp_layer_t& B0 = a->net[2].L[0];
   const drpo_mlp_layer_t& A1 = a->net[1].L[1];
   const drpo_mlp_layer_t& B1 = a->net[2].L[1];
+  // (the save pointers formed again after the barrier: held across the paired layer
+  // they cost it 64 spilled VGPRs)
+  const bool dA = DRPO_DEFER_HEADS && save_deferrable(A0.sy, A0.sz, A0.dout),
+             dB = DRPO_DEFER_HEADS && save_deferrable(B0.sy, B0.sz, B0.dout);
+  const GSave none{nullptr, nullptr, 0, 0};
   tile_dense_pair<FW_NW, RB, 4, ACT0, 16, 2>(T, LDH, 256, A0.W + (size_t)z * A0.wstride, A0.b + (size_t)z * A0.bstride,
                                           A0.dout, hA, B0.W + (size_t)z * B0.wstride, B0.b + (size_t)z * B0.bstride,
-                                          B0.dout, hB, LDH, layer_save(A0, z, a->rows, row0, nrows),
-                                          layer_save(B0, z, a->rows, row0, nrows));
+                                          B0.dout, hB, LDH, dA ? none : layer_save(A0, z, a->rows, row0, nrows),
+                                          dB ? none : layer_save(B0, z, a->rows, row0, nrows));
   lds_barrier();
+  if (dA) save_tile_lds<FW_NT, 16 * RB>(hA, LDH, layer_save(A0, z, a->rows, row0, nrows).gy, A0.dout, nrows);
+  if (dB) save_tile_lds<FW_NT, 16 * RB>(hB, LDH, layer_save(B0, z, a->rows, row0, nrows).gy, B0.dout, nrows);
   STAMP(5);
   tile_dense_narrow_pair<FW_NW, RB, ACT1>(hA, hB, LDH, A0.dout, A1.W + (size_t)z * A1.wstride,
                                           A1.b + (size_t)z * A1.bstride, A1.dout, o, B1.W + (size_t)z * B1.wstride,
@@ -366,14 +386,35 @@ __device__ __forceinline__ void pair_nets_nk(const drpo_mlp_net_t& A, const drpo
   auto W = [&](const drpo_mlp_layer_t& L) { return L.W + (size_t)z * L.wstride; };
   auto bb = [&](const drpo_mlp_layer_t& L) { return L.b + (size_t)z * L.bstride; };
   const drpo_mlp_layer_t &L0 = N.L[0], &L1 = N.L[1];
-  tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, NK0, 0, 2>(in, LDH, L0.din, W(L0), bb(L0), L0.dout, second ? bB : bA,
-                                                         LDH, layer_save(L0, z, rows, row0, nrows), nullptr, wl);
+  // deferred saves (save_tile_lds) only when both nets' layers defer: the whole
+  // workgroup stores both tiles after the barrier
+  const GSave none{nullptr, nullptr, 0, 0};
+  bool d;
+  {
+    const GSave s = layer_save(L0, z, rows, row0, nrows);
+    d = DRPO_DEFER_PAIR && save_deferrable(A.L[0].sy, A.L[0].sz, A.L[0].dout) &&
+        save_deferrable(B.L[0].sy, B.L[0].sz, B.L[0].dout);
+    tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, NK0, 0, 2>(in, LDH, L0.din, W(L0), bb(L0), L0.dout, second ? bB : bA,
+                                                           LDH, d ? none : s, nullptr, wl);
+  }
   lds_barrier();
+  if (d) {
+    save_tile_lds<FW_NT, 16 * RB>(bA, LDH, layer_save(A.L[0], z, rows, row0, nrows).gy, A.L[0].dout, nrows);
+    save_tile_lds<FW_NT, 16 * RB>(bB, LDH, layer_save(B.L[0], z, rows, row0, nrows).gy, B.L[0].dout, nrows);
+  }
   STAMP(2);
-  tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, 16, 0, 2>(second ? bB : bA, LDH, 256, W(L1), bb(L1), L1.dout,
-                                                        second ? T : in, LDH, layer_save(L1, z, rows, row0, nrows),
-                                                        nullptr, wl);
+  {
+    const GSave s = layer_save(L1, z, rows, row0, nrows);
+    d = DRPO_DEFER_PAIR && save_deferrable(A.L[1].sy, A.L[1].sz, A.L[1].dout) &&
+        save_deferrable(B.L[1].sy, B.L[1].sz, B.L[1].dout);
+    tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, 16, 0, 2>(second ? bB : bA, LDH, 256, W(L1), bb(L1), L1.dout,
+                                                          second ? T : in, LDH, d ? none : s, nullptr, wl);
+  }
   lds_barrier();
+  if (d) {
+    save_tile_lds<FW_NT, 16 * RB>(in, LDH, layer_save(A.L[1], z, rows, row0, nrows).gy, A.L[1].dout, nrows);
+    save_tile_lds<FW_NT, 16 * RB>(T, LDH, layer_save(B.L[1], z, rows, row0, nrows).gy, B.L[1].dout, nrows);
+  }
   STAMP(3);
   const drpo_mlp_layer_t &A2 = A.L[2], &B2 = B.L[2];
   tile_dense_narrow_pair<FW_NW, RB, ACT_NONE>(in, T, LDH, A2.din, W(A2), bb(A2), A2.dout, bA, W(B2), bb(B2), B2.dout,

@@ -19,7 +19,9 @@
 #include <stdlib.h>
 
 #define DRPO_UNIFORM_WEIGHT_LOADS 1   // scalar-base weight loads (see load_pk)
+#ifndef DRPO_PF_SCALE
 #define DRPO_PF_SCALE 12              // ring depth 6 for 2-block waves, 8 for 1-block waves
+#endif
 #include "common.hpp"
 #include "env_constraints.hpp"
 
@@ -433,7 +435,7 @@ __device__ __forceinline__ const float* step_opaque(const float* ptr) {
 #define DRPO_PERSIST_KARG 1   // config 2: 248 -> 242 us per launch (profiles/r03/ab_persist)
 #endif
 #ifndef DRPO_PREFETCH_M1
-#define DRPO_PREFETCH_M1 0
+#define DRPO_PREFETCH_M1 1   // member L1 weights fetched at the top of the step (profiles/r05/rollout_ab: +0.7-1.3 %)
 #endif
 #ifndef DRPO_ABIAS_LDS
 #define DRPO_ABIAS_LDS 0
