@@ -116,8 +116,8 @@ __device__ __forceinline__ void ff_epi_bwd(const f32x4 (&acc)[1][MAXC], int N, f
 #ifndef DRPO_FIT_PF
 #define DRPO_FIT_PF 6   // ring depth of the trunk-width (2 blocks per wave) layers
 #endif
-#ifndef DRPO_FIT_EPI_FIRST
-#define DRPO_FIT_EPI_FIRST 0   // A/B: a layer's epilogue before (1) or after (0) the next layer's prefetch
+#ifndef DRPO_FIT_DEFER
+#define DRPO_FIT_DEFER 0   // A/B macro (measured no gain, profiles/r05/fit_defer): coalesced saves after each barrier
 #endif
 constexpr int FPT = DRPO_FIT_PF;
 constexpr int FPH = 4;   // ring depth of the heads phase (3-4 blocks per wave)
@@ -324,7 +324,17 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   lds_barrier();
   FSTAMP(1);
 
+  // Saves for the weight gradients (layer inputs y, every dZ): with DRPO_FIT_DEFER the
+  // epilogues write LDS only and the whole workgroup stores the tile after the phase's
+  // barrier as 16-byte stores (save_tile_lds: a 200-float row in 50 lanes) instead of
+  // the accumulator layout's row-strided 4-byte stores.
+  auto dsave = [&](const float* buf, float* gy) {
+    if (DRPO_FIT_DEFER && gy) save_tile_lds<FF_NT, FF_ROWS>(buf, FF_LDH, gy, Hm, nrows);
+  };
+  auto esave = [&](float* gy) { return DRPO_FIT_DEFER ? nullptr : gy; };   // the epilogue's share
   // ---- trunk ------------------------------------------------------------------------
+  float* sy0 = tsave && t0.sy ? t0.sy + zr * Hm : nullptr;
+  float* sy1 = tsave && t1.sy ? t1.sy + zr * Hm : nullptr;
   {
     f32x4 acc[1][2];
     switch (nk1) {
@@ -335,14 +345,14 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
     }
     FSTAMP(10);
     float bv[2] = {bvt[0], bvt[1]};
-    if (DRPO_FIT_EPI_FIRST) ff_epi_fwd(acc, bv, Hm, T1, Z1, tsave && t0.sy ? t0.sy + zr * Hm : nullptr, Hm, nrows);
     ff_pre2<NK>(t1.W + (size_t)z * t1.wstride, NCB, bqt);
     ff_bias2(t1.b + (size_t)z * t1.bstride, Hm, bvt);
     FSTAMP(11);
-    if (!DRPO_FIT_EPI_FIRST) ff_epi_fwd(acc, bv, Hm, T1, Z1, tsave && t0.sy ? t0.sy + zr * Hm : nullptr, Hm, nrows);
+    ff_epi_fwd(acc, bv, Hm, T1, Z1, esave(sy0), Hm, nrows);
     FSTAMP(12);
   }
   lds_barrier();
+  dsave(T1, sy0);
   FSTAMP(2);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool second = wave >= FF_NW / 2;
@@ -355,17 +365,19 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   {
     f32x4 acc[1][2];
     ff_mma2<NK>(T1, t1.W + (size_t)z * t1.wstride, NCB, bqt, acc);
-    if (DRPO_FIT_EPI_FIRST) ff_epi_fwd(acc, bvt, Hm, T2, Z2, tsave && t1.sy ? t1.sy + zr * Hm : nullptr, Hm, nrows);
     ff_pre_heads<NK>(base, NCB, l0.W + (size_t)z * l0.wstride, l0.b + (size_t)z * l0.bstride, Hm,
                      l1.W + (size_t)z * l1.wstride, bqh, nbh, bvh);
-    if (!DRPO_FIT_EPI_FIRST) ff_epi_fwd(acc, bvt, Hm, T2, Z2, tsave && t1.sy ? t1.sy + zr * Hm : nullptr, Hm, nrows);
+    ff_epi_fwd(acc, bvt, Hm, T2, Z2, esave(sy1), Hm, nrows);
   }
   lds_barrier();
+  dsave(T2, sy1);
   FSTAMP(3);
   // ---- both heads: hidden + output layers, one phase ----------------------------------
   auto& Hb = Bd.net[1 + h];
   auto& o1 = Hb.L[1];
   auto& o0 = Hb.L[0];
+  auto& lown = F.net[1 + h].L[0];
+  float* syh = lown.sy ? lown.sy + zr * Hm : nullptr;   // this workgroup's head's hidden y
   {
     const bool own = (second ? 1 : 0) == h;
     const int nc = min(4, (NCB - base + 3) / 4);
@@ -373,20 +385,21 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
     const float* P = l0.W + (size_t)z * l0.wstride;
     float* out = second ? HB : HA;
     float* zb = own ? ZH : nullptr;
-    float* gy = own && l0.sy ? l0.sy + zr * Hm : nullptr;
+    float* gy = own ? esave(syh) : nullptr;
     const float* Pb1 = o1.W + (size_t)z * o1.wstride;
     if (nc == 4) ff_heads_core<4, NK>(base, T2, P, Hm, bqh, nbh, bvh, out, zb, gy, nrows, slot, Pb1, bqt);
     else ff_heads_core<3, NK>(base, T2, P, Hm, bqh, nbh, bvh, out, zb, gy, nrows, slot, Pb1, bqt);
   }
   lds_barrier();
+  dsave(h == 0 ? HA : HB, syh);
   FSTAMP(4);
   // ---- NLL (drpo_ens_loss's arithmetic; ens_upstream in csrc/mlp.hip) -------------------
+  float* Gd = T1;   // head h's output gradient (T1, the trunk's first layer y, is dead)
   {
     const int64_t nbx = (b + FF_ROWS - 1) / FF_ROWS;
     const float inv_n = 1.f / (float)(b * S1);
     const float gsc = (U.gscale ? *U.gscale : 1.f) * inv_n;
     float lacc = 0.f;
-    float* Gd = HA;   // head h's output gradient (HA's hidden y was saved above)
     if (tid < FF_ROWS * 16) {
       float gd = 0.f, gl = 0.f, cmn = 0.f, cmx = 0.f;
       if (nll) {
@@ -442,33 +455,40 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   // ---- backward: head h's hidden dZ, its trunk-L2 share, its trunk-L1 share ------------
   auto& tb = Bd.net[0].L[1];
   auto& ta = Bd.net[0].L[0];
+  float* dzh = o0.dz ? o0.dz + zr * Hm : nullptr;
+  float* dz2p = h == 0 ? tb.dz : tb.dz2;
+  float* dzt2 = dz2p ? dz2p + zr * Hm : nullptr;
+  float* dz1p = h == 0 ? ta.dz : ta.dz2;
+  float* dzt1 = dz1p ? dz1p + zr * Hm : nullptr;
   {
     f32x4 acc[1][2];
-    ff_mma2<1>(HA, o1.W + (size_t)z * o1.wstride, NCB, bqt, acc);   // K = S + 1 <= 16
+    ff_mma2<1>(Gd, o1.W + (size_t)z * o1.wstride, NCB, bqt, acc);   // K = S + 1 <= 16
     FSTAMP(13);
-    if (DRPO_FIT_EPI_FIRST) ff_epi_bwd(acc, Hm, HB, ZH, o0.dz ? o0.dz + zr * Hm : nullptr, Hm, nrows);
     ff_pre2<NK>(o0.W + (size_t)z * o0.wstride, NCB, bqt);
     FSTAMP(14);
-    if (!DRPO_FIT_EPI_FIRST) ff_epi_bwd(acc, Hm, HB, ZH, o0.dz ? o0.dz + zr * Hm : nullptr, Hm, nrows);
+    ff_epi_bwd(acc, Hm, HB, ZH, esave(dzh), Hm, nrows);
     FSTAMP(15);
   }
   lds_barrier();
+  dsave(HB, dzh);
   FSTAMP(6);
   {
     f32x4 acc[1][2];
     ff_mma2<NK>(HB, o0.W + (size_t)z * o0.wstride, NCB, bqt, acc);
-    float* d = h == 0 ? tb.dz : tb.dz2;
-    if (DRPO_FIT_EPI_FIRST) ff_epi_bwd(acc, Hm, HA, Z2, d ? d + zr * Hm : nullptr, Hm, nrows);
     ff_pre2<NK>(tb.W + (size_t)z * tb.wstride, NCB, bqt);
-    if (!DRPO_FIT_EPI_FIRST) ff_epi_bwd(acc, Hm, HA, Z2, d ? d + zr * Hm : nullptr, Hm, nrows);
+    ff_epi_bwd(acc, Hm, HA, Z2, esave(dzt2), Hm, nrows);
   }
   lds_barrier();
+  dsave(HA, dzt2);
   FSTAMP(7);
   {
     f32x4 acc[1][2];
     ff_mma2<NK>(HA, tb.W + (size_t)z * tb.wstride, NCB, bqt, acc);
-    float* d = h == 0 ? ta.dz : ta.dz2;
-    ff_epi_bwd(acc, Hm, nullptr, Z1, d ? d + zr * Hm : nullptr, Hm, nrows);
+    ff_epi_bwd(acc, Hm, DRPO_FIT_DEFER ? T1 : nullptr, Z1, esave(dzt1), Hm, nrows);
+  }
+  if (DRPO_FIT_DEFER) {
+    lds_barrier();
+    dsave(T1, dzt1);
   }
   FSTAMP(8);
 }
