@@ -2,11 +2,16 @@
 fixed sequence of HIP launches over engine-owned HBM workspaces.
 
 Per update_solver call (DRPO flags, actor on, multiplier on) the device runs:
-  sample_batch -> [critic] 8 fused MLP forwards/heads, critic_head (targets, losses,
-  output grads), 2 fused backward-data passes, 1 grouped weight-grad GEMM, clip +
-  Adam + EMA -> [actor] 7 forwards, upstream grads, 3 input-grad backwards, squash
-  backward, 1 backward + 1 weight-grad for both actors, clip + Adam (+ alpha) ->
-  [multiplier] 4 forwards, head, backward, weight-grad, clip + Adam.
+  sample_batch -> [critic] ONE multi-job forward ('c.f': the target critics and the
+  target certificate chained behind the policies on s' in the same workgroups, the
+  certificate on (s, a), the twin critics paired), ONE backward-data launch with the
+  critic / certificate losses formed in-kernel ('c.b1'), ONE grouped weight-gradient
+  launch (+ clip partials), ONE fused clip + Adam + EMA launch -> [actor] 'a.f1'
+  (actor + safe actor paired, rsample heads), 'a.f2' (critics at (s, a), (s, a_safe),
+  the certificate at tanh(mu_safe)), 'a.mult', 'a.b' (backward with the actor losses
+  formed in-kernel), 'a.bpi' (both squashed-Gaussian backwards), ONE weight-gradient
+  launch, ONE optimizer launch (+ alpha) -> [multiplier] 'm.f1', 'm.f2', 'm.mult',
+  multiplier_head, backward, weight-gradient, optimizer.
 All launch descriptors point at static workspaces, so they are built once per
 batch size and the whole sequence is graph-capturable. Noise: Philox in the
 kernels (production) or the reference's recorded draws (parity TapeNoise), which
