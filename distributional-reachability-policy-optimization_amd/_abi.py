@@ -137,7 +137,8 @@ class MlpFwd(ctypes.Structure):
                 ('nmean', P), ('nstd', P), ('save_x', P), ('net', MlpNet * 3), ('nnets', c_int), ('trunk', c_int),
                 ('rows', c_int64), ('nbatch', c_int), ('head', PolicyHead), ('split_heads', c_int),
                 ('ccb_out', P), ('ccb_dist', c_int), ('ccb_ratio', c_float), ('ccb_lmin', c_float), ('ccb_lmax', c_float),
-                ('pair', c_int), ('head2', PolicyHead), ('pre', MlpNet), ('pre_head', PolicyHead)]
+                ('pair', c_int), ('head2', PolicyHead), ('pre', MlpNet), ('pre_head', PolicyHead),
+                ('post', MlpNet), ('post_x', P)]
 
 
 class MlpBwdLayer(ctypes.Structure):

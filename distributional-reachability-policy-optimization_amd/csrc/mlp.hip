@@ -518,6 +518,29 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
           if (c == 0 || v > best) best = v;
         }
         a->ccb_out[(size_t)z * a->rows + row0 + tid] = best;
+        if (a->post.nl > 0) {   // the post chain's bound column (and its input save)
+          T[tid * LDH + c0] = best;
+          if (a->post_x) a->post_x[((size_t)z * a->rows + row0 + tid) * (c0 + 1) + c0] = best;
+        }
+      }
+      if (a->post.nl > 0) {
+        // post chain: the multiplier on [s, bound] (src/ssac.py:473-478,548-552) in this
+        // workgroup; its input assembled in T (the heads' first hidden tile, consumed),
+        // the bound's column written above by the thread that formed it
+        const int kp = round_up(c0 + 1, 16);
+        for (int e = tid; e < ROWS * kp; e += FW_NT) {
+          const int r = e / kp, k = e - r * kp;
+          if (k == c0) continue;
+          const int64_t row = row0 + r;
+          float v = 0.f;
+          if (r < nrows && k < c0) {
+            v = a->src[0][(size_t)z * a->sstride[0] + row * a->ld[0] + k];
+            if (a->post_x) a->post_x[((size_t)z * a->rows + row) * (c0 + 1) + k] = v;
+          }
+          T[r * LDH + k] = v;
+        }
+        lds_barrier();
+        run_net_g<RB>(a->post, a->rows, T, bA, bB, z, row0, nrows, red);
       }
     }
   } else {
@@ -603,6 +626,14 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
                        n2.L[0].din == 256 && n1.L[0].dout == n2.L[0].dout && n1.L[0].act == n2.L[0].act &&
                        n1.L[1].act == n2.L[1].act && n1.L[1].dout <= 16 && n2.L[1].dout <= 16,
                    "drpo_mlp_forward_multi: job %d: the constraint bound needs a trunk job with paired heads", j);
+    }
+    if (a->post.nl > 0) {
+      const drpo_mlp_net_t& pn = a->post;
+      DRPO_REQUIRE(a->ccb_out && a->cols[0] + 1 <= 64 && check_net(pn, a->cols[0] + 1) && !a->nmean,
+                   "drpo_mlp_forward_multi: job %d: a post chain needs the job's constraint bound (ccb_out) and a "
+                   "net on [src[0] (<= 63 columns), bound]", j);
+    } else {
+      DRPO_REQUIRE(!a->post_x, "drpo_mlp_forward_multi: job %d: post_x without a post net", j);
     }
     const int ns = (a->trunk || a->pair) ? 1 : a->nnets;
     DRPO_REQUIRE(slots + ns <= MJ_MAXSLOT, "drpo_mlp_forward_multi: too many nets");

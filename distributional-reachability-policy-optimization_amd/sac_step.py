@@ -18,6 +18,7 @@ kernels (production) or the reference's recorded draws (parity TapeNoise), which
 are consumed here in the reference's call order.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -126,6 +127,16 @@ def with_pre(d, policy, mode, A, eps, site, logp=None):
     fill_net(d.pre, policy)
     h = d.pre_head
     h.mode, h.A, h.eps, h.site, h.logp = mode, A, _p(eps), site, _p(logp)
+    return d
+
+
+def with_post(d, net, post_x=None):
+    """Post chain (drpo_mlp_fwd_t.post): `net` (the MLPMultiplier) runs after the job's
+    constraint bound (ccb_out), in the same workgroup, on [src[0] columns, bound]; its
+    layers save as any net's, post_x saves the assembled input (the multiplier update's
+    weight-gradient Y)."""
+    fill_net(d.post, net)
+    d.post_x = _p(post_x)
     return d
 
 
@@ -525,6 +536,11 @@ class SACEngine:
         d.ccb_ratio, d.ccb_lmin, d.ccb_lmax = float(cc.std_ratio), float(cc.log_std_min), float(cc.log_std_max)
         return d
 
+    def _post_mult(self):
+        """The multiplier forward as a post chain of the bound's job (csrc/mlp.hip,
+        drpo_mlp_fwd_t.post); DRPO_SAC_POST_MULT=0 keeps its own launch (A/B)."""
+        return self._ccb_fused() and os.environ.get('DRPO_SAC_POST_MULT', '1') != '0'
+
     def _cc_bound_after(self, name, out, dist):
         """drpo_cc_head over the saved head outputs of job `name` when _ccb could not fuse it."""
         if self._ccb_fused():
@@ -743,13 +759,22 @@ class SACEngine:
         self._run_multi('a.f1' + noise_tag(e5), jobs, ctr)
         # launch 2: Q_k(s, a), Qc(s, a), Qc(s, a_safe) with saves; Qc(s, tanh(mu_safe)) for lam
         qk = n['q0'] if k == 0 else n['q1']
-        self._run_multi(f'a.f2.{k}{int(mlp_mult)}', lambda: [
+        # lam = multiplier(s, bound) chained behind the bound in the same workgroups (no
+        # 'a.mult' launch) when the bound is formed in-kernel
+        post = mlp_mult and self._post_mult()
+
+        def ccm():
+            d = self._ccb(fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True),
+                          self.buf('a.sqc', B), dist)
+            return with_post(d, self._out_net(n['mult'], 'a.multx', B)) if post else d
+        # (job order = workgroup dispatch order; the chained job last measured faster here,
+        # first in m.f2: profiles/r05/post_mult)
+        self._run_multi(f'a.f2.{k}{int(mlp_mult)}{int(post)}', lambda: [
             fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
             fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True),
-            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)] + ([
-            self._ccb(fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True),
-                      self.buf('a.sqc', B), dist)] if mlp_mult else []), ctr)
-        if mlp_mult:
+            fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)] + (
+            [ccm()] if mlp_mult else []), ctr)
+        if mlp_mult and not post:
             # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad); the bound is formed
             # by the forward launch above
             sqc = self.buf('a.sqc', B)
@@ -911,14 +936,21 @@ class SACEngine:
         self._run_multi('m.f1' + noise_tag(e7), jobs, ctr)
         # launch 2: constraint critic at (s, a) and at (s, tanh(mu_safe))
         aqc, sqc = self.buf('m.aqc', B), self.buf('m.sqc', B)
-        self._run_multi('m.f2', lambda: [
-            self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc, dist),
-            self._ccb(fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True), sqc,
-                      dist)], ctr)
+        xm = self.buf('m.x', B, S + 1)
+        post = self._post_mult()   # the multiplier chained behind the bound at tanh(mu_safe)
+
+        def ccs():
+            d = self._ccb(fill_fwd(self._outs_cc('m.ccs'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True), sqc,
+                          dist)
+            return with_post(d, n['mult'], xm) if post else d
+        self._run_multi(f'm.f2{int(post)}', lambda: [
+            ccs(), self._ccb(fill_fwd(self._outs_cc('m.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True), aqc,
+                             dist)], ctr)
         self._cc_bound_after('m.cc', aqc, dist)
         self._cc_bound_after('m.ccs', sqc, dist)
-        xm = self.buf('m.x', B, S + 1)
-        self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B, save_x=xm))
+        if not post:
+            self._run_fwd('m.mult', lambda: fill_fwd([n['mult']], [(self.bs, S), (sqc, 1), (None, 0)], B,
+                                                     save_x=xm))
         gx = self.buf('m.gx', B)
         mc = sol.mlp_multiplier_cfg
         _lib.check(L.drpo_multiplier_head(B, n['mult'].sy[-1].data_ptr(), sqc.data_ptr(), aqc.data_ptr(),

@@ -181,6 +181,11 @@ typedef struct {
                           next-state policy feeding the target critics / certificate
                           (src/ssac.py:284-294,387-400) without a launch or an HBM round trip */
   drpo_policy_head_t pre_head;
+  drpo_mlp_net_t post; /* post chain (post.nl > 0; a trunk job with ccb_out): a net run after the bound in
+                          the same workgroup on [src[0] columns (cols[0] wide), the bound] -- the
+                          MLPMultiplier lam(s, max_C Qc_ub(s, a)) of src/ssac.py:473-478,548-552
+                          without its own launch; its layer saves as any net's */
+  float* post_x;       /* optional save of the post net's assembled input [rows][cols[0] + 1] */
 } drpo_mlp_fwd_t;
 
 typedef struct {
