@@ -514,3 +514,37 @@ def test_fit_fb_matches_two_launches(c):
             np.testing.assert_allclose(a, b, rtol=0, atol=1e-4 * float(np.abs(b).max()) + 1e-30, err_msg=k)
         else:
             np.testing.assert_allclose(a, b, rtol=2e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize('c', [2])
+def test_multiplier_post_chain_matches_separate_launch(c):
+    """The MLPMultiplier forward chained behind the constraint bound in the same
+    workgroups (drpo_mlp_fwd_t.post: no 'a.mult' / 'm.mult' launch) against its own
+    launch (DRPO_SAC_POST_MULT=0), at the reference widths (256: the bound is formed
+    in-kernel): the same layers on the same [s, bound] rows, so two actor and two
+    multiplier updates leave bitwise the same parameters."""
+    import os
+    from drpo_amd.rng import DeviceNoise
+
+    def run(post):
+        os.environ['DRPO_SAC_POST_MULT'] = '1' if post else '0'
+        alg, cd = _alg(c, B=1024)
+        sol = alg.solver
+        assert sol.mlp_multiplier
+        g = torch.Generator().manual_seed(5)
+        noise = DeviceNoise(11)
+        for _ in range(2):
+            obs = torch.randn(1024, alg.state_dim, generator=g).to(DEV)
+            sol.update_actor_and_alpha(obs, noise=noise)
+            sol.update_multiplier(obs, noise=noise)
+        torch.cuda.synchronize()
+        assert sol.engine._ccb_fused() and sol.engine._post_mult() == post
+        return {k: v.detach().clone() for k, v in sol.state_dict().items()}
+
+    try:
+        a = run(True)
+        b = run(False)
+    finally:
+        os.environ.pop('DRPO_SAC_POST_MULT', None)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k

@@ -145,3 +145,4 @@ def test_actor_arena_rebuild_matches_presized_engine():
     assert rebuilt_a, 'B = 5000 must outgrow the arena sized for the solver batch'
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
