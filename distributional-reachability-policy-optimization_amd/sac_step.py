@@ -539,7 +539,8 @@ class SACEngine:
     def _post_mult(self):
         """The multiplier forward as a post chain of the bound's job (csrc/mlp.hip,
         drpo_mlp_fwd_t.post); DRPO_SAC_POST_MULT=0 keeps its own launch (A/B)."""
-        return self._ccb_fused() and os.environ.get('DRPO_SAC_POST_MULT', '1') != '0'
+        return (self._ccb_fused() and self.S + 1 <= 64 and self.nets['mult'].layers[0][2] == self.S + 1 and
+                os.environ.get('DRPO_SAC_POST_MULT', '1') != '0')
 
     def _cc_bound_after(self, name, out, dist):
         """drpo_cc_head over the saved head outputs of job `name` when _ccb could not fuse it."""
