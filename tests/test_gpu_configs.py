@@ -206,7 +206,12 @@ def _check_params(sol, P, msg, grads=None, lr=3e-4, atol=3e-5, rtol=1e-4):
         if fail.any():
             bad.append((k, float(np.abs(got - e).max()), int(fail.sum()), e.size))
     assert not bad, f'{msg}: {bad[:6]}'
-    assert weak <= 1e-4 * sum(v.numel() for v in P.values()) + 8, f'{msg}: {weak} ill-conditioned elements'
+    total = sum(v.numel() for v in P.values())
+    assert weak <= 1e-4 * total + 8, f'{msg}: {weak} ill-conditioned elements'
+    if weak:   # reported in the run's warnings summary (the carve-out's count, per check)
+        import warnings
+        warnings.warn(f'{msg}: {weak} of {total} elements inside the 2 lr ill-conditioned carve-out')
+    return weak
 
 
 @pytest.mark.parametrize('c', CFGS)
