@@ -187,7 +187,7 @@ class CriticHead(ctypes.Structure):
                 ('log_alpha', P), ('r', P), ('h', P), ('d', P), ('dc', P), ('q0t', P), ('q1t', P), ('logp2', P),
                 ('mu_t', P), ('ls_t', P), ('eps3', P), ('seed', c_uint64), ('ctr', c_uint64),
                 ('q0', P), ('q1', P), ('mu', P), ('ls', P), ('dq0', P), ('dq1', P), ('dmu', P), ('dls', P),
-                ('loss', P), ('loss_part', P)]
+                ('loss', P), ('loss_part', P), ('cost', c_int), ('v', P)]
 
 
 class WgradAdam(ctypes.Structure):

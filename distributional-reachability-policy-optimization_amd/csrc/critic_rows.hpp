@@ -67,9 +67,16 @@ __device__ __forceinline__ float cert_element(const Head& p, int64_t i, int c, f
   // certificate-target done flags: the batch's, or the model-predicted ones of the
   // robust branch (src/ssac.py:387-400)
   const float dnc = p.dc ? (gload(p.dc + i) ? 1.f : 0.f) : dn;
-  const float hv = gload(p.h + k);
   const float mu = gload(p.mu + k);
   const float mut = gload(p.mu_t + k);
+  if (p.cost) {
+    // cost certificate (src/ssac.py:306-310): one-step discounted violation cost, MSE
+    const float yc = (gload(p.v + i) ? 1.f : 0.f) + p.discount * (1.f - dn) * mut;
+    dmu = 2.f * (mu - yc) * invN;
+    dls = 0.f;
+    return (mu - yc) * (mu - yc) * invN;
+  }
+  const float hv = gload(p.h + k);
   const float lst = p.distributional ? gload(p.ls_t + k) : 0.f;
   const float lsk = p.distributional ? gload(p.ls + k) : 0.f;
   float q2;

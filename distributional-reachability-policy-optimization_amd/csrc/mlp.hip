@@ -1439,6 +1439,8 @@ static int bwd_multi_launch(const drpo_mlp_bwd_t* jobs_host, const drpo_mlp_bwd_
       continue;
     }
     DRPO_REQUIRE(head && J.nbatch == 1 && J.rows == head->B, "drpo_mlp_backward_multi: job %d needs the critic head", j);
+    DRPO_REQUIRE(!head->cost || (head->v && !head->distributional),
+                 "drpo_mlp_backward_multi: cost target needs v, not distributional");
     if (J.upstream == DRPO_UPSTREAM_CRITIC)
       DRPO_REQUIRE(!J.trunk && J.nnets == 2 && J.net[0].L[J.net[0].nl - 1].dout == 1 &&
                        J.net[1].L[J.net[1].nl - 1].dout == 1,

@@ -235,6 +235,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(drpo_critic_head_t p) 
 DRPO_API int drpo_critic_head(const drpo_critic_head_t* p, drpo_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DRPO_REQUIRE(p && p->C >= 1 && p->B >= 0, "drpo_critic_head: bad descriptor");
+  DRPO_REQUIRE(!p->cost || (p->v && !p->distributional), "drpo_critic_head: cost target needs v, not distributional");
   if (p->B == 0) return DRPO_OK;
   critic_head_kernel<<<(unsigned)((p->B + 63) / 64), 64, 0, stream>>>(*p);
   DRPO_LAUNCH_CHECK("critic_head");

@@ -281,13 +281,17 @@ class SACEngine:
     def __init__(self, solver):
         self.sol = solver
         self.profiler = None
-        self.S, self.A, self.C = solver.state_dim, solver.action_dim, solver.con_dim
+        # C: the constraint critic's output width (con_dim, or 1 for the cost certificate);
+        # Ch: the constraint values' width (the batch's h)
+        self.S, self.A, self.C = solver.state_dim, solver.action_dim, solver.constraint_critic.output_dim
+        self.Ch = solver.con_dim
+        self.cost = solver.constrained_fcn == 'cost'
         self.dev = solver.actor.group.data.device
         from .distributed import GradReducer
         self.dp = GradReducer()
         from .envs import device_env_params
         self.env_params = device_env_params(solver.env) if solver.qc_under_uncertainty and \
-            not solver.distributional_qc else None
+            not solver.distributional_qc and not self.cost else None
         self.B = None
         self.ws = {}
         self.wg_ws = {}
@@ -390,7 +394,7 @@ class SACEngine:
             net.sy[-1] = buf(f'{key}.out', B, net.dout)
         # batch
         self.bs, self.ba, self.bs2 = buf('b.s', B, S), buf('b.a', B, A), buf('b.s2', B, S)
-        self.br, self.bh = buf('b.r', B), buf('b.h', B, C)
+        self.br, self.bh = buf('b.r', B), buf('b.h', B, self.Ch)
         self.bd, self.bv = buf('b.d', B, dtype=torch.uint8), buf('b.v', B, dtype=torch.uint8)
         # noise buffers (parity mode)
         for k, shp in (('em', (B, S + 1)), ('e1', (B, A)), ('e2', (B, A)), ('e3', (B, C)), ('e5', (B, A)), ('e6', (B, A)),
@@ -579,7 +583,7 @@ class SACEngine:
             dst.copy_(src.reshape(dst.shape))
         self.bd.copy_(done.reshape(B).to(torch.uint8))
         self.bv.copy_(violation.reshape(B).to(torch.uint8))
-        self.bh.copy_(constraint_value.reshape(B, self.C))
+        self.bh.copy_(constraint_value.reshape(B, self.Ch))
         return self._critic_step(noise)
 
     def _critic_step(self, noise):
@@ -588,7 +592,7 @@ class SACEngine:
         self.noise = noise = noise or self.noise
         L = _lib.lib()
         dist = sol.distributional_qc and sol.qc_under_uncertainty
-        robust = sol.qc_under_uncertainty and not sol.distributional_qc
+        robust = sol.qc_under_uncertainty and not sol.distributional_qc and not self.cost
         qshape = (B,) if C == 1 else (B, C)
         e1 = self._eps('e1', noise.normal((B, A)))
         if robust:
@@ -627,11 +631,13 @@ class SACEngine:
         # workgroup for both twins) at (s, a) with their backward saves, and the targets with
         # their next-state policies chained in (drpo_mlp_fwd_t.pre): a'_safe ~ pi_safe(s')
         # (robust: the model's s') -> target certificate at (s', a'_safe); a' ~ pi(s') with
-        # log pi -> target twins at (s', a') (src/ssac.py:284-294,304-400)
+        # log pi -> target twins at (s', a') (src/ssac.py:284-294,304-400). The cost certificate
+        # draws its next action from the actor instead (src/ssac.py:306-310).
         pq = pairable(n['q0'], n['q1'])
+        tpol = n['actor' if self.cost else 'safe']
         self._run_multi('c.f' + rk + noise_tag(e1), lambda: [
             with_pre(fill_fwd(self._cc_nets('t'), [(s2c, S), (None, A), (None, 0)], B, trunk=True),
-                     Net(n['safe'].layers), HEAD_SAMPLE, A, e2, SITE_SAFE_NEXT),
+                     Net(tpol.layers), HEAD_SAMPLE, A, e2, SITE_SAFE_NEXT),
             with_pre(fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (None, A), (None, 0)], B, pair=pq),
                      Net(n['actor'].layers), HEAD_SAMPLE, A, e1, SITE_PI_NEXT, logp=lp2),
             fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
@@ -656,6 +662,7 @@ class SACEngine:
         ch.log_alpha = sol.log_alpha.data_ptr()
         ch.eps3 = _p(e3)
         ch.dc = ws['c.dm'].data_ptr() if robust else 0
+        ch.cost, ch.v = int(self.cost), self.bv.data_ptr()
         ch.seed, ch.ctr = noise.seed, ctr
         ch.loss = loss.data_ptr()
         # per-16-row-tile loss partials (twin 0 | twin 1 | certificate), summed into
@@ -732,7 +739,9 @@ class SACEngine:
             noise.randn_like(qshape, used=False)       # Qc(s, a)
             if mlp_mult:
                 noise.randn_like(qshape, used=False)   # Qc(s, tanh(mu_safe)) for lambda
-        e6 = self._eps('e6', noise.std_normal((B, A)))
+        # the cost certificate has no safe-actor loss (src/ssac.py:488-494): no a_safe draw
+        cost = self.cost
+        e6 = None if cost else self._eps('e6', noise.std_normal((B, A)))
         if dist:
             noise.randn_like(qshape, used=False)
         ctr = noise.next()
@@ -744,8 +753,19 @@ class SACEngine:
         raw, raws = n['actor'].sy[-1], n['safe'].sy[-1]
         # launch 1: actor and safe actor rsample (saves for backward) + fused heads
         # (one workgroup runs both policies when their shapes pair: the same input, one
-        # saved copy of it)
-        if pairable(n['actor'], n['safe']):
+        # saved copy of it). Cost certificate: the safe actor only gives tanh(mu_safe) for the
+        # multiplier's input (src/ssac.py:473-478), or nothing without the MLP multiplier.
+        if cost:
+            jobs = lambda: [
+                with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
+                                             save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
+                                    e=e),
+                          HEAD_MEAN, A, None, 0, amean=am, second=True)] if mlp_mult and pairable(n['actor'], n['safe']) \
+                else [with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE,
+                                A, e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e)] + (
+                    [with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A,
+                               None, 0, amean=am)] if mlp_mult else [])
+        elif pairable(n['actor'], n['safe']):
             jobs = lambda: [
                 with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
                                              save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
@@ -771,8 +791,8 @@ class SACEngine:
         # (job order = workgroup dispatch order; the chained job last measured faster here,
         # first in m.f2: profiles/r05/post_mult)
         self._run_multi(f'a.f2.{k}{int(mlp_mult)}{int(post)}', lambda: [
-            fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True),
-            fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True),
+            fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True)] + (
+            [] if cost else [fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True)]) + [
             fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)] + (
             [ccm()] if mlp_mult else []), ctr)
         if mlp_mult and not post:
@@ -808,28 +828,29 @@ class SACEngine:
         # dL/da of the actor (Q_k part + certificate part, summed in the squash backward in
         # the reference's order) and of the safe actor: one backward launch
         dA, dAc, dAs = self.buf('a.dA', B, A), self.buf('a.dAc', B, A), self.buf('a.dAs', B, A)
-        hv, hv2 = self.nets_view['a.cc'], self.nets_view['a.cc2']
+        hv, hv2 = self.nets_view['a.cc'], self.nets_view.get('a.cc2')
         gq, gmu, gls, gmu2, gls2 = (self.buf('a.gq', B), self.buf('a.gmu', B, C), self.buf('a.gls', B, C),
                                     self.buf('a.gmu2', B, C), self.buf('a.gls2', B, C))
         self._run_bwd_multi(f'a.b.{k}{int(dist)}', lambda: [
             fill_bwd(hv if dist else hv[:2], [None, gmu, gls][:3 if dist else 2], B, trunk=True,
-                     dx={0: (dAc, S, A, False)}, upstream=UPSTREAM_ACTOR_CC),
+                     dx={0: (dAc, S, A, False)}, upstream=UPSTREAM_ACTOR_CC)] + ([] if cost else [
             fill_bwd(hv2 if dist else hv2[:2], [None, gmu2, gls2][:3 if dist else 2], B, trunk=True,
-                     dx={0: (dAs, S, A, False)}, upstream=UPSTREAM_SAFE_CC),
+                     dx={0: (dAs, S, A, False)}, upstream=UPSTREAM_SAFE_CC)]) + [
             fill_bwd([self.nets_view[f'a.q{k}']], [gq], B, dx={0: (dA, S, A, False)}, upstream=UPSTREAM_NEG_MEAN)],
             actor=ah)
         draw, draws = self.buf('a.draw', B, 2 * A), self.buf('a.draws', B, 2 * A)
         asum = self.alpha_sum
         self._clean_grads(sol.actor.group)
-        self._clean_grads(sol.actor_safe.group)
-        self._run_bwd_multi('a.bpi', lambda: [fill_bwd([n['actor']], [draw], B, upstream=UPSTREAM_SQUASH),
-                                              fill_bwd([n['safe']], [draws], B, upstream=UPSTREAM_SQUASH_SAFE)],
-                            actor=ah)
+        if not cost:
+            self._clean_grads(sol.actor_safe.group)
+        self._run_bwd_multi('a.bpi', lambda: [fill_bwd([n['actor']], [draw], B, upstream=UPSTREAM_SQUASH)] + (
+            [] if cost else [fill_bwd([n['safe']], [draws], B, upstream=UPSTREAM_SQUASH_SAFE)]), actor=ah)
         na, ns = n['actor'], n['safe']
-        sq = self._sq('a', ('a', 's'))
+        asegs = ('a',) if cost else ('a', 's')
+        sq = self._sq('a', asegs)
         used = self._run_wgrad('a.wg' + ('f' if sq else ''),
-                               lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]], 'a'),
-                                                    (ns, [xa, ns.sy[0], ns.sy[1]], 's')], B, sq))
+                               lambda: wgrad_items([(na, [xa, na.sy[0], na.sy[1]], 'a')] + (
+                                   [] if cost else [(ns, [xa, ns.sy[0], ns.sy[1]], 's')]), B, sq))
         # d alpha_loss / d log_alpha = -exp(log_alpha) * mean(logp + target_entropy) is formed
         # inside the optimizer launch from the alpha-loss sum (src/ssac.py:498-501); under
         # DP the sum is sum-reduced and divided by G*B rows (same value: log_alpha is
@@ -839,7 +860,7 @@ class SACEngine:
         # actor: clip + Adam + cosine; alpha: Adam (no wd, fixed lr); safe actor: clip + Adam +
         # cosine -- one fused optimizer launch (clip partials from the weight gradients)
         ga, gs = sol.actor.group, sol.actor_safe.group
-        pa, ps = self._clip_parts(used if sq else None, 'a', ('a', 's'), [ga.grad, gs.grad])
+        pa, *ps = self._clip_parts(used if sq else None, 'a', asegs, [ga.grad, gs.grad][:len(asegs)])
         aopt = sol.alpha_optimizer
         if aopt.tensor is None:
             aopt.tensor = sol.log_alpha.view(1)
@@ -853,14 +874,16 @@ class SACEngine:
             segs.append(aopt.segment(0, 1, aopt.step_scalars(), grad=asum[:1],
                                      grad_from_sum=(asum, B * self.dp.world, (B + 15) // 16),
                                      grad_from_sum_kind=2 if sol.use_log_alpha_loss else 0))
-        segs.append(sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
-                                                     clip=(ps, sol.grad_norm) if safe_full else None, zero_grad=True,
-                                                     pack_map=gs.pack_map(), grad_scale=gsc))
+        if not cost:   # the cost certificate's optimizer list is [actor, alpha] (src/ssac.py:509-513)
+            segs.append(sol.actor_safe_optimizer.segment(0, gs.size, sol.actor_safe_optimizer.step_scalars(),
+                                                         clip=(ps[0], sol.grad_norm) if safe_full else None,
+                                                         zero_grad=True, pack_map=gs.pack_map(), grad_scale=gsc))
         fused_step(segs)
         self._grads_zeroed(ga)
-        self._grads_zeroed(gs)
+        if not cost:
+            self._grads_zeroed(gs)
         sol.actor_lr_scheduler.step()
-        if safe_full:
+        if safe_full and not cost:
             sol.actor_safe_lr_scheduler.step()
 
     def _alpha_adam(self, grad):
@@ -1035,7 +1058,7 @@ class SACEngine:
 
         rv, vv = view(rb, False), view(vb, True)
         L = _lib.lib()
-        _lib.check(L.drpo_sample_batch(ctypes.byref(rv), ctypes.byref(vv), n_real, B, self.S, self.A, self.C,
+        _lib.check(L.drpo_sample_batch(ctypes.byref(rv), ctypes.byref(vv), n_real, B, self.S, self.A, self.Ch,
                                        None if ir is None else self.ws['idx_r'].data_ptr(),
                                        None if iv is None else self.ws['idx_v'].data_ptr(), noise.seed, ctr,
                                        float(alg.reward_scale), float(alg.alive_bonus), float(alg.constraint_scale),

@@ -171,8 +171,15 @@ class SSAC(Module):
             setattr(self, k, v)
         if isinstance(self.target_entropy, Optional):
             self.target_entropy = None
-        assert self.constrained_fcn == 'reachability', \
-            "constrained_fcn='cost' is out of scope (the reachability certificate is the DRPO hot path)"
+        assert self.constrained_fcn in ('reachability', 'cost'), self.constrained_fcn
+        if self.constrained_fcn == 'cost':
+            # the reference's cost branch runs only where it does not crash: compute_cons_target
+            # returns one target, which the distributional loss unpacks as two (src/ssac.py:430-431),
+            # and _get_qc of the single-output critic asserts for con_dim > 1 behind the MLP
+            # multiplier (src/ssac.py:476,548)
+            assert not self.distributional_qc, "constrained_fcn='cost' needs distributional_qc=False"
+            assert con_dim == 1 or not self.mlp_multiplier, \
+                "constrained_fcn='cost' with con_dim > 1 needs mlp_multiplier=False"
         self.state_dim, self.action_dim, self.con_dim = state_dim, action_dim, con_dim
         self.horizon = horizon
         self.violation_cost = 0.0
@@ -192,7 +199,10 @@ class SSAC(Module):
 
         cg = FlatGroup('critic')
         critic = CriticEnsemble(self.critic_cfg, state_dim, action_dim, prefix='critic.')
-        cc = ConstraintCritic(self.constraint_critic_cfg, state_dim, action_dim, con_dim,
+        # certificate width: one output per constraint, or one cost value (src/ssac.py:191-195;
+        # the reference's softplus output_activation is accepted and ignored there, :55-62)
+        cc_out = con_dim if self.constrained_fcn == 'reachability' else 1
+        cc = ConstraintCritic(self.constraint_critic_cfg, state_dim, action_dim, cc_out,
                               prefix='constraint_critic.')
         critic.register(cg)
         cc.register(cg)
@@ -214,7 +224,7 @@ class SSAC(Module):
         cc.build(cg, 'constraint_critic.')
         critic_t = CriticEnsemble(self.critic_cfg, state_dim, action_dim, prefix='critic.')
         critic_t.build(tg, 'critic.')
-        cc_t = ConstraintCritic(self.constraint_critic_cfg, state_dim, action_dim, con_dim,
+        cc_t = ConstraintCritic(self.constraint_critic_cfg, state_dim, action_dim, cc_out,
                                 prefix='constraint_critic.')
         cc_t.build(tg, 'constraint_critic.')
         self.critic, self.critic_target = critic, critic_t

@@ -322,6 +322,10 @@ typedef struct {
   float* loss_part;   /* drpo_mlp_backward_multi_head only: per-workgroup loss partials instead of
                          atomics into loss: [3][row tiles] = twin 0, twin 1, certificate (summed by
                          a drpo_mlp_wgrad_sums reduction) */
+  /* constrained_fcn='cost' (src/ssac.py:306-310): certificate target = violation + discount *
+     (1 - done) * mu_t, MSE loss (distributional must be 0); v = the batch's violation flags */
+  int cost;
+  const uint8_t* v;
 } drpo_critic_head_t;
 
 int drpo_mlp_forward(const drpo_mlp_fwd_t* desc /* host */, drpo_stream_t stream);

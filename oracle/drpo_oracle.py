@@ -547,9 +547,13 @@ class SSACOracle:
                       multiplier_lr=3e-4, multiplier_lr_end=1e-5, distributional=True, uncertainty=True,
                       deterministic_backup=False, target_entropy=-float(A), batch_size=256,
                       updates_per_training=1000, actor_update_interval=2, multiplier_update_interval=5,
-                      mlp_multiplier=True, fixed_multiplier=15.0, autotune_alpha=True, use_log_alpha_loss=False)
+                      mlp_multiplier=True, fixed_multiplier=15.0, autotune_alpha=True, use_log_alpha_loss=False,
+                      cost=False)
         self.c.update(cfg)
-        self.C, self.A = C, A
+        if self.c.get('constrained_fcn') == 'cost':
+            self.c['cost'] = True
+        # the cost certificate is one value per row (src/ssac.py:191)
+        self.C, self.A = (1 if self.c['cost'] else C), A
         c = self.c
         T = c['updates_per_training']
         self.opt = {g: {} for g in ['critic', 'actor', 'actor_safe', 'multiplier', 'alpha']}
@@ -589,11 +593,16 @@ class SSACOracle:
                 nv = nv - self.alpha.detach() * logp
             return r + self.c['discount'] * (1. - d.float()) * nv
 
-    # --- src/ssac.py:304-413 (reachability; distributional or vanilla)
-    def compute_cons_target(self, s, a, s2, d, h, rng, P=None):
+    # --- src/ssac.py:304-413 (reachability; distributional or vanilla; or the cost certificate)
+    def compute_cons_target(self, s, a, s2, d, h, rng, P=None, v=None):
         P = self.P if P is None else P
         g, C = self.c['discount'], self.C
         with torch.no_grad():
+            if self.c['cost']:
+                # src/ssac.py:306-310: a' ~ pi(s'), Qc_target(s', a'), one-step violation cost
+                a2, _, _, _ = policy_sample(P, 'actor.net.', s2, rng)
+                q2 = cons_critic(P, 'constraint_critic_target.', s2, a2, 'mean')
+                return v.float() + g * (1. - d.float()) * q2, None
             robust = self.c['uncertainty'] and not self.c['distributional']
             if not robust:
                 a2, _, _, _ = policy_sample(P, 'actor_safe.net.', s2, rng)
@@ -622,7 +631,7 @@ class SSACOracle:
     def update_critic(self, s, a, s2, r, d, v, h, rng):
         """src/ssac.py:437-456."""
         y = self.compute_target(s2, r, d, rng)
-        yc, yb = self.compute_cons_target(s, a, s2, d, h, rng)
+        yc, yb = self.compute_cons_target(s, a, s2, d, h, rng, v=v)
         dist = self.c['distributional']
         rs = rng
 
@@ -681,8 +690,9 @@ class SSACOracle:
 
         ka = self.keys(['actor.'])
         _, ga = self._grad(actor_loss, ka)
-        # safe actor loss draws after the actor loss (src/ssac.py:488-494)
-        kas = self.keys(['actor_safe.'])
+        # safe actor loss draws after the actor loss (src/ssac.py:488-494); the cost
+        # certificate has none (optimizers [actor, alpha], src/ssac.py:509-513)
+        kas = [] if self.c['cost'] else self.keys(['actor_safe.'])
 
         def safe_loss(Q):
             a_s, _, _, _ = policy_rsample(Q, 'actor_safe.net.', s, rng)
@@ -692,7 +702,7 @@ class SSACOracle:
         # alpha, or log_alpha itself with use_log_alpha_loss
         coef = 1.0 if self.c['use_log_alpha_loss'] else self.alpha
         alpha_grad = -coef * torch.mean(store['logp'] + self.c['target_entropy'])
-        _, gs = self._grad(safe_loss, kas)
+        gs = self._grad(safe_loss, kas)[1] if kas else {}
         clip_grads([ga[k] for k in ka], self.c['grad_norm'])
         lr = self.sched['actor'].lr
         for k in ka:
@@ -706,12 +716,12 @@ class SSACOracle:
             self.log_alpha = la
         # the reference clips / schedules the safe actor at optimizer index 2, which is
         # the safe actor only when the alpha optimizer sits at index 1 (src/ssac.py:515-527)
-        if auto:
+        if auto and kas:
             clip_grads([gs[k] for k in kas], self.c['grad_norm'])
         lr = self.sched['actor_safe'].lr
         for k in kas:
             adam_update(self.opt['actor_safe'], k, self.P[k], gs[k], lr, 1e-4)
-        if auto:
+        if auto and kas:
             self.sched['actor_safe'].step()
 
     def update_multiplier(self, s, rng):

@@ -404,6 +404,19 @@ def gen_solver_flags(out):
         gen_ssac(out, name, seed, tag, dist, unc, extra)
 
 
+# constrained_fcn='cost' (src/ssac.py:191-195,306-310): the reference runs it with
+# distributional_qc=False only, and behind the MLP multiplier only for con_dim == 1
+COST_CASES = [
+    ('point-robot', 44, 'cost_point', False, True, {'constrained_fcn': 'cost'}),
+    ('quadrotor', 45, 'cost_quad', False, False, {'constrained_fcn': 'cost', 'mlp_multiplier': False}),
+]
+
+
+def gen_cost(out):
+    for name, seed, tag, dist, unc, extra in COST_CASES:
+        gen_ssac(out, name, seed, tag, dist, unc, extra)
+
+
 def gen_smbpo_update(out, name, seed):
     cfg = small_config(name, B=32, H=3, sac_batch=32)
     alg = build_alg(name, cfg, seed)
@@ -653,6 +666,9 @@ def main():
     if sys.argv[1:] == ['solver_flags']:
         gen_solver_flags(out)
         return
+    if sys.argv[1:] == ['cost']:
+        gen_cost(out)
+        return
     if sys.argv[1:] == ['robust']:
         gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
         gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
@@ -669,6 +685,7 @@ def main():
     gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
     gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
     gen_solver_flags(out)
+    gen_cost(out)
     gen_smbpo_update(out, 'point-robot', 41)
     gen_smbpo_update(out, 'quadrotor', 42)
     gen_trainer(out, 55)

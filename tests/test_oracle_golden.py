@@ -151,7 +151,7 @@ def ssac_cfg(d):
 
 
 SSAC_TAGS = ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point', 'scalar_mult_point',
-             'scalar_mult_quad', 'fixed_alpha_quad', 'log_alpha_point']
+             'scalar_mult_quad', 'fixed_alpha_quad', 'log_alpha_point', 'cost_point', 'cost_quad']
 
 
 @pytest.mark.parametrize('tag', SSAC_TAGS)
