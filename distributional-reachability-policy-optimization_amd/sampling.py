@@ -93,12 +93,17 @@ def sample_episodes_batched(env, policy, n_traj, eval=False, safe_shield_thresho
 def stat_forwards(solver, states, actions, distributional, mlp_multiplier):
     """Q / Qc / Qc-std / lambda of SMBPO.log_statistics (src/smbpo.py:369-399) for one
     row set: critic mean, constraint-critic mean (max over C), its std, the safe actor's
-    certificate and the multiplier on it."""
+    certificate and the multiplier on it. The cost certificate reports its raw mean and
+    no lambda (the reference's reachability-only branches, src/smbpo.py:380-398)."""
     out = {'q': solver.critic.mean(states, actions)}
     cc = solver.constraint_critic
-    out['qc'] = solver._get_qc(cc(states, actions))
+    reach = solver.constrained_fcn == 'reachability'
+    qc = cc(states, actions)
+    out['qc'] = solver._get_qc(qc) if reach else qc
     if distributional:
         out['qc_std'] = ops.constraint_critic_forward(cc, states, actions, sample=True, noise=_NO_TAPE)[1]
+    if not reach:
+        return out
     a_safe = solver.actor_safe.act(states, eval=True).detach()
     safe_qcs = solver._get_qc(cc(states, a_safe))
     if mlp_multiplier:

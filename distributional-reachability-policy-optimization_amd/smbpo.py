@@ -387,7 +387,7 @@ class SMBPO(Configurable, Module):
                 mean_q, mean_qc = st['q'].mean(), st['qc'].mean()
                 if cfg.distributional_qc:
                     mean_qc_std = st['qc_std'].mean()
-                if cfg.mlp_multiplier:
+                if 'lam' in st:
                     mean_lam = st['lam'].mean()
             log.message(f'Average Q {which}: {mean_q}')
             self.data.append(f'Average Q {which}', mean_q)

@@ -415,12 +415,19 @@ COST_CASES = [
 def gen_cost(out):
     for name, seed, tag, dist, unc, extra in COST_CASES:
         gen_ssac(out, name, seed, tag, dist, unc, extra)
+    # two rollout_and_update() calls through the device batch path (violation flags
+    # gathered from the buffers)
+    gen_smbpo_update(out, 'point-robot', 46, 'cost_point', False, {'constrained_fcn': 'cost'})
 
 
-def gen_smbpo_update(out, name, seed):
-    cfg = small_config(name, B=32, H=3, sac_batch=32)
+def gen_smbpo_update(out, name, seed, tag=None, distributional=True, sac_extra=None):
+    cfg = small_config(name, B=32, H=3, sac_batch=32, distributional=distributional)
+    if sac_extra:
+        cfg.update({'sac_cfg': dict(sac_extra)})
     alg = build_alg(name, cfg, seed)
     d = meta(name, cfg, alg)
+    for k, v in (sac_extra or {}).items():
+        d['flag/' + k] = np.array(v)
     d.update(sd_dict(alg, 'sd0/'))
     d['sd0/log_alpha'] = t2n(alg.solver.log_alpha)
     d.update(fill_replay(alg, name, 300, seed + 1, alg.con_dim))
@@ -441,7 +448,7 @@ def gen_smbpo_update(out, name, seed):
         d['virt/' + k] = t2n(v)
     d['losses/critic'] = np.array([float(x) for x in alg.recent_critic_losses])
     d['losses/cons'] = np.array([float(x) for x in alg.recent_cons_critic_losses])
-    np.savez_compressed(os.path.join(out, f'smbpo_update_{name}.npz'), **d)
+    np.savez_compressed(os.path.join(out, f'smbpo_update_{tag or name}.npz'), **d)
 
 
 class RecordingPointRobot(PointRobot):

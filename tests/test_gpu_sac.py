@@ -77,11 +77,14 @@ def test_ssac_updates_match_reference(tag):
     np.testing.assert_array_equal(np.array(lrs), d['lr3'])
 
 
-@pytest.mark.parametrize('env', ['point-robot', 'quadrotor'])
-def test_rollout_and_update_matches_reference(env):
+@pytest.mark.parametrize('tag', ['point-robot', 'quadrotor', 'cost_point'])
+def test_rollout_and_update_matches_reference(tag):
     """Two full SMBPO.rollout_and_update() calls (rollout + 10 update_solver each, the
-    reference cadence) from the post-fit state of the fixture."""
-    d = load_golden(f'smbpo_update_{env}')
+    reference cadence) from the post-fit state of the fixture. cost_point: the
+    constrained_fcn='cost' certificate through the device batch path (violation flags
+    gathered from the buffers)."""
+    d = load_golden(f'smbpo_update_{tag}')
+    env = str(d['meta/env'])
     alg = small_smbpo(d, env)
     sd1 = {k[len('sd1/'):]: torch.from_numpy(np.array(d[k])) for k in d.files if k.startswith('sd1/')}
     la = sd1.pop('log_alpha', None)

@@ -199,9 +199,10 @@ def smbpo_cfg(d):
                            holdout=int(d['meta/model_batch']), num_elites=int(d['meta/num_elites'])))
 
 
-@pytest.mark.parametrize('env', ['point-robot', 'quadrotor'])
-def test_smbpo_update(env):
-    d = load_golden(f'smbpo_update_{env}')
+@pytest.mark.parametrize('tag', ['point-robot', 'quadrotor', 'cost_point'])
+def test_smbpo_update(tag):
+    d = load_golden(f'smbpo_update_{tag}')
+    env = str(d['meta/env'])
     full = sd(d, 'sd0/')
     la = full.pop('log_alpha')
     full['solver.log_alpha'] = la
