@@ -586,7 +586,7 @@ class SACEngine:
         self.bh.copy_(constraint_value.reshape(B, self.Ch))
         return self._critic_step(noise)
 
-    def _critic_step(self, noise):
+    def _critic_step(self, noise, early_actor=False):
         sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
         self._ensure_packed()
         self.noise = noise = noise or self.noise
@@ -635,13 +635,17 @@ class SACEngine:
         # draws its next action from the actor instead (src/ssac.py:306-310).
         pq = pairable(n['q0'], n['q1'])
         tpol = n['actor' if self.cost else 'safe']
-        self._run_multi('c.f' + rk + noise_tag(e1), lambda: [
+        # early_actor: the following actor update's first forward (actor / safe-actor
+        # rsample, independent of the critic update) rides in this launch as its shortest
+        # job, drawing its Philox noise at this launch's counter (device noise only)
+        self._run_multi('c.f' + rk + noise_tag(e1) + ('+a' if early_actor else ''), lambda: [
             with_pre(fill_fwd(self._cc_nets('t'), [(s2c, S), (None, A), (None, 0)], B, trunk=True),
                      Net(tpol.layers), HEAD_SAMPLE, A, e2, SITE_SAFE_NEXT),
             with_pre(fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (None, A), (None, 0)], B, pair=pq),
                      Net(n['actor'].layers), HEAD_SAMPLE, A, e1, SITE_PI_NEXT, logp=lp2),
             fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
-            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)], ctr)
+            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)] + (
+            self._actor_f1_jobs(None, None) if early_actor else []), ctr)
         loss = self._loss_slots(2)
         self._clean_grads(sol.critic_group)
         ch = self.desc.get('c.head')
@@ -724,7 +728,7 @@ class SACEngine:
         self.bs.copy_(obs)
         return self._actor_step(noise)
 
-    def _actor_step(self, noise):
+    def _actor_step(self, noise, f1_done=False):
         sol, n, B, S, A, C = self.sol, self.nets, self.B, self.S, self.A, self.C
         self._ensure_packed()
         self.noise = noise = noise or self.noise
@@ -750,34 +754,10 @@ class SACEngine:
         a, lp, u, e = self.buf('a.a', B, A), self.buf('a.lp', B), self.buf('a.u', B, A), self.buf('a.e', B, A)
         a_s, u_s, e_s, am = self.buf('a.as', B, A), self.buf('a.us', B, A), self.buf('a.es', B, A), \
             self.buf('a.am', B, A)
-        raw, raws = n['actor'].sy[-1], n['safe'].sy[-1]
-        # launch 1: actor and safe actor rsample (saves for backward) + fused heads
-        # (one workgroup runs both policies when their shapes pair: the same input, one
-        # saved copy of it). Cost certificate: the safe actor only gives tanh(mu_safe) for the
-        # multiplier's input (src/ssac.py:473-478), or nothing without the MLP multiplier.
-        if cost:
-            jobs = lambda: [
-                with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
-                                             save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
-                                    e=e),
-                          HEAD_MEAN, A, None, 0, amean=am, second=True)] if mlp_mult and pairable(n['actor'], n['safe']) \
-                else [with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE,
-                                A, e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e)] + (
-                    [with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A,
-                               None, 0, amean=am)] if mlp_mult else [])
-        elif pairable(n['actor'], n['safe']):
-            jobs = lambda: [
-                with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
-                                             save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
-                                    e=e),
-                          HEAD_RSAMPLE, A, e6, SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am, second=True)]
-        else:
-            jobs = lambda: [
-                with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE,
-                          A, e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e),
-                with_head(fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A, e6,
-                          SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am)]
-        self._run_multi('a.f1' + noise_tag(e5), jobs, ctr)
+        # launch 1: actor and safe actor rsample (saves for backward) + fused heads, unless
+        # the critic update's forward launch already ran them (early_actor)
+        if not f1_done:
+            self._run_multi('a.f1' + noise_tag(e5), lambda: self._actor_f1_jobs(e5, e6), ctr)
         # launch 2: Q_k(s, a), Qc(s, a), Qc(s, a_safe) with saves; Qc(s, tanh(mu_safe)) for lam
         qk = n['q0'] if k == 0 else n['q1']
         # lam = multiplier(s, bound) chained behind the bound in the same workgroups (no
@@ -885,6 +865,48 @@ class SACEngine:
         sol.actor_lr_scheduler.step()
         if safe_full and not cost:
             sol.actor_safe_lr_scheduler.step()
+
+    def _early_actor(self, noise):
+        """The actor update's first forward joins the critic update's forward launch:
+        production (Philox) noise only -- a recorded tape hands over the actor's draws
+        after the critic's -- and DRPO_SAC_EARLY_ACTOR=0 keeps the separate 'a.f1' launch."""
+        return not getattr(noise, 'parity', False) and os.environ.get('DRPO_SAC_EARLY_ACTOR', '1') != '0'
+
+    def _actor_f1_jobs(self, e5, e6):
+        """The actor update's first forward (src/ssac.py:459-461,489-490): actor and safe
+        actor rsample with saves for the backward, and tanh(mu_safe), as multi-job forward
+        jobs (launched alone as 'a.f1', or appended to the critic update's 'c.f')."""
+        sol, n, B, S, A = self.sol, self.nets, self.B, self.S, self.A
+        cost, mlp_mult = self.cost, sol.mlp_multiplier
+        xa = self.buf('a.x', B, S)   # the actors' shared input save (the wgrad's first-layer Y of both)
+        a, lp, u, e = self.buf('a.a', B, A), self.buf('a.lp', B), self.buf('a.u', B, A), self.buf('a.e', B, A)
+        a_s, u_s, e_s, am = self.buf('a.as', B, A), self.buf('a.us', B, A), self.buf('a.es', B, A), \
+            self.buf('a.am', B, A)
+        # One workgroup runs both policies when their shapes pair (the same input, one
+        # saved copy of it). Cost certificate: the safe actor only gives tanh(mu_safe) for the
+        # multiplier's input (src/ssac.py:473-478), or nothing without the MLP multiplier.
+        if cost:
+            return [
+                with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
+                                             save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
+                                    e=e),
+                          HEAD_MEAN, A, None, 0, amean=am, second=True)] if mlp_mult and pairable(n['actor'], n['safe']) \
+                else [with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE,
+                                A, e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e)] + (
+                    [with_head(fill_fwd([Net(n['safe'].layers)], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_MEAN, A,
+                               None, 0, amean=am)] if mlp_mult else [])
+        elif pairable(n['actor'], n['safe']):
+            return [
+                with_head(with_head(fill_fwd([n['actor'], n['safe']], [(self.bs, S), (None, 0), (None, 0)], B,
+                                             save_x=xa, pair=True), HEAD_RSAMPLE, A, e5, SITE_PI_RS, a=a, logp=lp, u=u,
+                                    e=e),
+                          HEAD_RSAMPLE, A, e6, SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am, second=True)]
+        else:
+            return [
+                with_head(fill_fwd([n['actor']], [(self.bs, S), (None, 0), (None, 0)], B, save_x=xa), HEAD_RSAMPLE,
+                          A, e5, SITE_PI_RS, a=a, logp=lp, u=u, e=e),
+                with_head(fill_fwd([n['safe']], [(self.bs, S), (None, 0), (None, 0)], B), HEAD_RSAMPLE, A, e6,
+                          SITE_SAFE_RS, a=a_s, u=u_s, e=e_s, amean=am)]
 
     def _alpha_adam(self, grad):
         opt = self.sol.alpha_optimizer
@@ -1065,9 +1087,10 @@ class SACEngine:
                                        float(alg.constraint_offset), self.bs.data_ptr(), self.ba.data_ptr(),
                                        self.bs2.data_ptr(), self.br.data_ptr(), self.bd.data_ptr(),
                                        self.bv.data_ptr(), self.bh.data_ptr(), _lib.stream()), 'sample_batch')
-        lq, lqc = self._critic_step(noise)
+        early = update_actor and self._early_actor(noise)
+        lq, lqc = self._critic_step(noise, early_actor=early)
         if update_actor:
-            self._actor_step(noise)
+            self._actor_step(noise, f1_done=early)
         if update_multiplier:
             self._mult_step(noise)
         return lq, lqc

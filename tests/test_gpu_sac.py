@@ -152,3 +152,47 @@ def test_actor_arena_rebuild_matches_presized_engine():
     for k in a:
         assert torch.equal(a[k], b[k]), k
 
+
+
+@pytest.mark.parametrize('tag', ['drpo_quad', 'cost_point'])
+def test_early_actor_forward_matches_standalone_launch(tag):
+    """Production noise: the actor update's first forward rides in the critic update's
+    forward launch ('c.f+a', SACEngine._early_actor). Its outputs (actions, log-probs,
+    pre-tanh samples and noise, tanh(mu_safe), every saved activation) must be bitwise
+    those of the stand-alone 'a.f1' launch at the same Philox counter, and the critic
+    update must be unchanged by the extra job."""
+    from drpo_amd.rng import DeviceNoise
+    d = load_golden(f'ssac_{tag}')
+    env = str(d['meta/env'])
+    batch = [torch.from_numpy(d['in/' + k]).to(DEV) for k in ['s', 'a', 's2', 'r', 'd', 'v', 'h']]
+
+    def run(early):
+        alg = small_smbpo(d, env)
+        sol = alg.solver
+        sd0 = solver_sd(d, 'sd0/')
+        sol.log_alpha.fill_(float(sd0.pop('log_alpha')))
+        sol.load_state_dict(sd0, strict=False)
+        eng = sol.engine
+        orig = eng._critic_step
+        eng._critic_step = lambda nz: orig(nz, early_actor=early)
+        noise = DeviceNoise(11)
+        lq, lqc = sol.update_critic(*batch, noise=noise)
+        torch.cuda.synchronize()
+        return sol, eng, noise.ctr, (lq.item(), lqc.item())
+
+    sol, eng, ctr, losses = run(True)
+    names = ['a.a', 'a.lp', 'a.u', 'a.e', 'a.am', 'a.x'] + ([] if eng.cost else ['a.as', 'a.us', 'a.es'])
+    nets = [eng.nets['actor']] + ([] if eng.cost else [eng.nets['safe']])
+    early = [eng.ws[k].clone() for k in names] + [y.clone() for n in nets for y in n.sy if y is not None]
+    for t in [eng.ws[k] for k in names] + [y for n in nets for y in n.sy if y is not None]:
+        t.fill_(float('nan'))
+    eng._run_multi('a.f1.test', lambda: eng._actor_f1_jobs(None, None), ctr)
+    torch.cuda.synchronize()
+    alone = [eng.ws[k] for k in names] + [y for n in nets for y in n.sy if y is not None]
+    for i, (x, y) in enumerate(zip(early, alone)):
+        assert torch.equal(x, y), f'output {i} differs'
+    sol2, _, _, losses2 = run(False)
+    assert losses == losses2
+    ref = sol2.state_dict()
+    for k, v in sol.state_dict().items():
+        assert torch.equal(v, ref[k]), k
