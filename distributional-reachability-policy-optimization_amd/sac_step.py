@@ -73,6 +73,15 @@ def _p(t):
     return 0 if t is None else t.data_ptr()
 
 
+def _job_order(key, jobs):
+    """A/B knob: DRPO_SAC_REVERSE = comma-separated launch-key prefixes whose job lists
+    (= workgroup dispatch order) are reversed."""
+    rev = os.environ.get('DRPO_SAC_REVERSE', '')
+    if rev and any(key.startswith(p) for p in rev.split(',') if p):
+        return jobs[::-1]
+    return jobs
+
+
 def noise_tag(eps):
     """descriptor-cache suffix: recorded draws (parity) vs Philox (production)"""
     return '.p' if eps is not None else '.d'
@@ -438,7 +447,7 @@ class SACEngine:
         built once and kept in device memory."""
         d = self.desc.get(key)
         if d is None:
-            jobs = builder()
+            jobs = _job_order(key, builder())
             arr = (MlpFwd * len(jobs))(*jobs)
             d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(fwd_flops(j) for j in jobs))
         arr, dev, nj, fl = d
@@ -450,7 +459,7 @@ class SACEngine:
     def _run_bwd_multi(self, key, builder, head=None, actor=None):
         d = self.desc.get(key)
         if d is None:
-            jobs = builder()
+            jobs = _job_order(key, builder())
             arr = (MlpBwd * len(jobs))(*jobs)
             d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(bwd_flops(j) for j in jobs))
         arr, dev, nj, fl = d
@@ -638,14 +647,24 @@ class SACEngine:
         # early_actor: the following actor update's first forward (actor / safe-actor
         # rsample, independent of the critic update) rides in this launch as its shortest
         # job, drawing its Philox noise at this launch's counter (device noise only)
-        self._run_multi('c.f' + rk + noise_tag(e1) + ('+a' if early_actor else ''), lambda: [
-            with_pre(fill_fwd(self._cc_nets('t'), [(s2c, S), (None, A), (None, 0)], B, trunk=True),
-                     Net(tpol.layers), HEAD_SAMPLE, A, e2, SITE_SAFE_NEXT),
-            with_pre(fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (None, A), (None, 0)], B, pair=pq),
-                     Net(n['actor'].layers), HEAD_SAMPLE, A, e1, SITE_PI_NEXT, logp=lp2),
-            fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
-            fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)] + (
-            self._actor_f1_jobs(None, None) if early_actor else []), ctr)
+        # Job order = workgroup dispatch order. Measured (profiles/r05/early_actor): without
+        # the actor jobs, chains first (96.5 us; plain first 100.4); with them, actor, plain,
+        # chains (104.7 us; actor, chains, plain 111.4; chains, plain, actor 119.5).
+        # DRPO_SAC_EARLY_FIRST / DRPO_SAC_CF_PLAIN_FIRST override (A/B).
+        early_first = early_actor and os.environ.get('DRPO_SAC_EARLY_FIRST', '1') == '1'
+        plain_first = os.environ.get('DRPO_SAC_CF_PLAIN_FIRST', '1' if early_actor else '0') == '1'
+
+        def cf_jobs():
+            chains = [with_pre(fill_fwd(self._cc_nets('t'), [(s2c, S), (None, A), (None, 0)], B, trunk=True),
+                               Net(tpol.layers), HEAD_SAMPLE, A, e2, SITE_SAFE_NEXT),
+                      with_pre(fill_fwd([n['q0t'], n['q1t']], [(self.bs2, S), (None, A), (None, 0)], B, pair=pq),
+                               Net(n['actor'].layers), HEAD_SAMPLE, A, e1, SITE_PI_NEXT, logp=lp2)]
+            plain = [fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
+                     fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)]
+            actor = self._actor_f1_jobs(None, None) if early_actor else []
+            main = plain + chains if plain_first else chains + plain
+            return actor + main if early_first else main + actor
+        self._run_multi('c.f' + rk + noise_tag(e1) + ('+a' if early_actor else ''), cf_jobs, ctr)
         loss = self._loss_slots(2)
         self._clean_grads(sol.critic_group)
         ch = self.desc.get('c.head')
@@ -768,13 +787,13 @@ class SACEngine:
             d = self._ccb(fill_fwd(self._outs_cc('a.ccm'), [(self.bs, S), (am, A), (None, 0)], B, trunk=True),
                           self.buf('a.sqc', B), dist)
             return with_post(d, self._out_net(n['mult'], 'a.multx', B)) if post else d
-        # (job order = workgroup dispatch order; the chained job last measured faster here,
-        # first in m.f2: profiles/r05/post_mult)
-        self._run_multi(f'a.f2.{k}{int(mlp_mult)}{int(post)}', lambda: [
-            fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True)] + (
-            [] if cost else [fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True)]) + [
+        # (job order = workgroup dispatch order: the multiplier's chained job, Q_k, then the
+        # certificate jobs measured 86.8 us against 90.9 us for the reverse order
+        # (profiles/r05/early_actor/order); m.f2 keeps its chained job first)
+        self._run_multi(f'a.f2.{k}{int(mlp_mult)}{int(post)}', lambda: ([ccm()] if mlp_mult else []) + [
             fill_fwd([self._reuse(qk, f'a.q{k}')], [(self.bs, S), (a, A), (None, 0)], B)] + (
-            [ccm()] if mlp_mult else []), ctr)
+            [] if cost else [fill_fwd(self._reuse_cc('a.cc2'), [(self.bs, S), (a_s, A), (None, 0)], B, trunk=True)]) + [
+            fill_fwd(self._reuse_cc('a.cc'), [(self.bs, S), (a, A), (None, 0)], B, trunk=True)], ctr)
         if mlp_mult and not post:
             # lam = multiplier(s, max_C Qc_ub(s, tanh(mu_safe)))  (no grad); the bound is formed
             # by the forward launch above
