@@ -191,26 +191,27 @@ def with_head(d, mode, A, eps, site, a=None, logp=None, u=None, e=None, amean=No
     return d
 
 
-def wgrad_items(entries, rows, sq=None):
+def wgrad_items(entries, rows, sq=None, key=None):
     """entries: [(net, inputs_per_layer[, segment])] -> (ctypes array of WgradItem, count,
     {segment: partial slots used}). With sq = {segment: device tensor}, every item of a
     segment writes the sums of squares of its finished gradient tiles into consecutive
     slots of that segment's tensor (the clip partials of drpo_optim_step)."""
     L = _lib.lib()
     items, used = [], {}
-    for ent in entries:
-        net, ins = ent[0], ent[1]
-        seg = ent[2] if len(ent) > 2 else None
-        for l, (W, b, din, dout, act, WT) in enumerate(net.layers):
-            gW, gb = net.grad_layers[l]
-            it = WgradItem()
-            it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
-            it.dout, it.din, it.rows, it.nbatch = dout, din, rows, 1
-            if sq is not None and seg is not None:
-                it.sq, it.sq_off = sq[seg].data_ptr(), used.get(seg, 0)
-                used[seg] = it.sq_off + L.drpo_mlp_wgrad_tiles(ctypes.byref(it))
-                assert used[seg] <= sq[seg].numel(), 'clip partial buffer too small'
-            items.append(it)
+    units = [(ent[0], ent[1], ent[2] if len(ent) > 2 else None, l) for ent in entries for l in range(len(ent[0].layers))]
+    if key is not None:
+        units = _job_order(key, units)   # A/B knob (item order = dispatch order)
+    for net, ins, seg, l in units:
+        W, b, din, dout, act, WT = net.layers[l]
+        gW, gb = net.grad_layers[l]
+        it = WgradItem()
+        it.dz, it.y, it.gW, it.gb = net.dz[l].data_ptr(), ins[l].data_ptr(), gW.data_ptr(), gb.data_ptr()
+        it.dout, it.din, it.rows, it.nbatch = dout, din, rows, 1
+        if sq is not None and seg is not None:
+            it.sq, it.sq_off = sq[seg].data_ptr(), used.get(seg, 0)
+            used[seg] = it.sq_off + L.drpo_mlp_wgrad_tiles(ctypes.byref(it))
+            assert used[seg] <= sq[seg].numel(), 'clip partial buffer too small'
+        items.append(it)
     arr = (WgradItem * len(items))(*items)
     return arr, len(items), used
 
@@ -706,7 +707,7 @@ class SACEngine:
         if dist:
             items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]], 'cc'))
         sq = self._sq('c', ('c', 'cc'))
-        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq),
+        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq, key='c.wg'),
                                sums=[(lpart[:2 * nt], loss[0]), (lpart[2 * nt:], loss[1])])
         cg = sol.critic_group
         self.dp.sum_(cg.grad)      # the 1/G of the mean rides in the optimizer segments
