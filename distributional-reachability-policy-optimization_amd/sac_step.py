@@ -649,9 +649,11 @@ class SACEngine:
         # rsample, independent of the critic update) rides in this launch as its shortest
         # job, drawing its Philox noise at this launch's counter (device noise only)
         # Job order = workgroup dispatch order. Measured (profiles/r05/early_actor): without
-        # the actor jobs, chains first (96.5 us; plain first 100.4); with them, actor, plain,
-        # chains (104.7 us; actor, chains, plain 111.4; chains, plain, actor 119.5).
-        # DRPO_SAC_EARLY_FIRST / DRPO_SAC_CF_PLAIN_FIRST override (A/B).
+        # the actor jobs, q pair, certificate, qt chain, cc_t chain (94.3 us; cc_t, qt, cc, q
+        # 97.2; cc, q, cc_t, qt 100.4); with them, actor, certificate, q pair, cc_t, qt
+        # (105.5 us; actor, q, cc, qt, cc_t 112.9; actor, chains, plain 111.4; chains, plain,
+        # actor 119.5). DRPO_SAC_EARLY_FIRST / _CF_PLAIN_FIRST / _CF_REVERSED /
+        # _CFA_REVERSED override (A/B).
         early_first = early_actor and os.environ.get('DRPO_SAC_EARLY_FIRST', '1') == '1'
         plain_first = os.environ.get('DRPO_SAC_CF_PLAIN_FIRST', '1' if early_actor else '0') == '1'
 
@@ -664,6 +666,10 @@ class SACEngine:
                      fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)]
             actor = self._actor_f1_jobs(None, None) if early_actor else []
             main = plain + chains if plain_first else chains + plain
+            if not early_actor and os.environ.get('DRPO_SAC_CF_REVERSED', '1') == '1':
+                main = main[::-1]          # q pair, certificate, target chains
+            elif early_actor and os.environ.get('DRPO_SAC_CFA_REVERSED', '0') == '1':
+                main = plain[::-1] + chains[::-1]
             return actor + main if early_first else main + actor
         self._run_multi('c.f' + rk + noise_tag(e1) + ('+a' if early_actor else ''), cf_jobs, ctr)
         loss = self._loss_slots(2)
