@@ -296,6 +296,43 @@ def cpu_baseline(cfgd, seed, budget_s=16.0):
                               f'B={Bs}, 4 threads'}}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """Run this script as `torch.distributed.run --nproc-per-node n` in a child
+    process (one rank per GPU, rendezvous on 127.0.0.1). The ranks' JSON result line
+    (printed by rank 0 only) is relayed to stdout and everything else to stderr; the
+    return code is torchrun's, which is non-zero when any rank failed."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    result = []
+    for line in p.stdout:
+        if line.startswith('{') and '"metric"' in line:
+            result.append(line)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = p.wait()
+    for line in result:
+        sys.stdout.write(line)
+    sys.stdout.flush()
+    if rc == 0 and len(result) != 1:
+        sys.stderr.write(f'bench.py: expected one result line from {n} ranks, got {len(result)}\n')
+        return 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -319,7 +356,13 @@ def main():
     ap.add_argument('--engine', type=int, default=0, help='rollout engine: 0 auto (fused horizon), 1 per-step launches')
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside torchrun: start the N ranks as fresh child
+        # processes before this process touches the GPU (no exec), relay rank 0's line
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU')
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
@@ -348,6 +391,8 @@ def main():
         B = args.batch or cfgd['B']
     custom = any(x is not None for x in (args.batch, args.horizon, args.ensemble, args.global_batch))
     label = cfgd['label'] if not custom else f'{env} E={E} H={H} B={B}/rank (custom shape, not a BASELINE config)'
+    if gb is not None and not custom:
+        label += f', B={B} per rank on {world} rank(s)'
 
     import drpo_amd  # noqa: F401
     from drpo_amd.ops import EventTimer

@@ -112,6 +112,23 @@ def test_bench_two_ranks_gloo():
     assert res['model_fit']['sharding'].startswith('members')
 
 
+def test_bench_gpus_flag_launches_ranks():
+    """a plain `bench.py --gpus 2` (no torchrun wrapper) starts the 2
+    ranks itself and prints rank 0's single line with n_gpus 2."""
+    import json
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), 'bench.py'), '--gpus', '2', '--backend', 'gloo',
+           '--steps', '2', '--warmup', '1', '--fit-steps', '2', '--no-cpu-baseline']
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res['n_gpus'] == 2 and res['config']['parallelism'] == 'dp2'
+    assert res['value'] > 0 and res['sac']['value'] > 0
+    assert res['model_fit']['sharding'].startswith('members')
+
+
 @pytest.mark.parametrize('mode', ['batch', 'members'])
 def test_dp_collection_replicas_agree(mode):
     """step_generator past buffer_min + model fits under DP (2 ranks, gloo,
