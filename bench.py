@@ -354,6 +354,7 @@ def main():
                     help="steps of the timed fit call (default: the config's model_steps, the length of "
                          "the reference's fit(steps=) call, src/smbpo.py:214-216)")
     ap.add_argument('--engine', type=int, default=0, help='rollout engine: 0 auto (fused horizon), 1 per-step launches')
+    ap.add_argument('--elites', default=None, help='comma-separated elite members (traffic probes)')
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -402,8 +403,8 @@ def main():
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
     alg.model_ensemble.state_normalizer.fit(alg.replay_buffer.get('states'))
     steady_mode(alg)
-    if os.environ.get('DRPO_BENCH_ELITES'):   # traffic probe: the elite set the rollout draws from
-        alg.model_ensemble._elite_inds = [int(x) for x in os.environ['DRPO_BENCH_ELITES'].split(',')]
+    if args.elites:   # traffic probe: the elite set the rollout draws from
+        alg.model_ensemble._elite_inds = [int(x) for x in args.elites.split(',')]
     from drpo_amd.distributed import sync_parameters
     sync_parameters(alg)            # every rank starts from rank 0's weights (DP replicas)
     do_sac = not args.rollout_only
@@ -414,7 +415,6 @@ def main():
     from drpo_amd import _lib as dlib
     # production noise: ops.rollout picks the fused engine (2) for H <= 128
     fused_engine = args.engine == 2 or (args.engine == 0 and H <= 128)
-    fused_engine = fused_engine and os.environ.get('DRPO_BENCH_TORCH_PHASE') != '1'   # A/B: torch phase events
 
     def one_step(tmr):
         if tmr is not None and fused_engine:

@@ -297,57 +297,27 @@ struct GSave {
 // bias values of this lane's output columns, loaded before the k-loop so their
 // latency hides behind it (loaded after the loop they cost a full L2 round trip
 // per layer)
-// (The rollout's DRPO_ABIAS_LDS A/B build stages the actor biases in LDS; only that
-// build carries the address-space test, so default builds keep one plain global load.)
 template <int NW, int MAXC>
 __device__ __forceinline__ void load_bias(const float* __restrict__ bias, int N, float (&bv)[MAXC]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int col = (wave + NW * c) * 16 + (lane & 15);
-#if defined(DRPO_ABIAS_LDS) && DRPO_ABIAS_LDS
-    if (bias && __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)bias)) {   // LDS-staged
-      bv[c] = col < N ? ((const __attribute__((address_space(3))) float*)(bias))[col] : 0.f;
-      continue;
-    }
-#endif
     bv[c] = (bias && col < N) ? gload(bias + col) : 0.f;
   }
 }
 
-// LDS stores of MFMA accumulators. A 16x16 accumulator's register r holds row 4g + r
-// (g = lane >> 4) of column lane & 15, and ds_write_b32 banks a wave's 64 lanes in two
-// 32-lane groups by dword address mod 32 (MI355X_MICROARCH.md, LDS). With a row stride
-// == 8 (mod 32) (lds_ld: the A-fragment reads' conflict-free stride) lane groups g = 2h
-// and 2h + 1 of one store land on the SAME 16 banks (rows 4 apart: 32 dwords): a 2-way
-// conflict on every epilogue store -- the 24.9 % "bank conflict" cycles of the SAC
-// forward's PMC (profiles/r04/pmc_sac). A 2-way conflict on ds_write_b32 fits inside the
-// store's own 4-cycle transfer, so it costs no time; the conflict-free order below (lanes
-// of odd g store register r ^ 2, row 4g + (r ^ 2): 16 banks away; r ^ 1 for the
-// 16-float-stride partial slabs) costs a lane select per store and measured SLOWER on
-// one box, alternating (profiles/r05/swz_ab: rollout frac 0.434-0.435 vs 0.466, SAC 63.5
-// vs 65.7 TFLOP/s, fit 0.0757 vs 0.0735 ms). Kept as an A/B macro, off.
-#ifndef DRPO_PROBE_NOSAVE
-#define DRPO_PROBE_NOSAVE 0   // timing probes only: the MLP epilogues skip their global saves (results wrong)
-#endif
-#ifndef DRPO_LDS_SWZ
-#define DRPO_LDS_SWZ 0   // A/B macro, measured slower (profiles/r05/swz_ab): off
-#endif
-template <int X>
-__device__ __forceinline__ int swz_row(int r, int g) { return DRPO_LDS_SWZ ? r ^ (X * (g & 1)) : r; }
-template <int X>
-__device__ __forceinline__ float swz_pick(const f32x4& v, int r, int g) {
-  return (DRPO_LDS_SWZ && (g & 1)) ? v[r ^ X] : v[r];
-}
+// LDS stores of MFMA accumulators: a 16x16 accumulator's register r holds row 4g + r
+// (g = lane >> 4) of column lane & 15. With a row stride == 8 (mod 32) (lds_ld) lane
+// groups g = 2h and 2h + 1 of one ds_write_b32 land on the same 16 banks: a 2-way
+// conflict that fits inside the store's own 4-cycle transfer (MI355X_MICROARCH.md, LDS),
+// so it costs no time. (A conflict-free swizzled order measured slower: profiles/r05/swz_ab.)
 
 // A layer's [rows][N] output tile saved to global from LDS after the layer's barrier,
 // as 16-byte stores by every thread of the workgroup (at N = 256 one wave-instruction
 // writes one whole 1 KB row) instead of the epilogue's row-strided 4-byte stores (four
-// 64 B pieces per wave-instruction, 4x the store instructions): DRPO_DEFER_SAVES.
+// 64 B pieces per wave-instruction, 4x the store instructions).
 // N % 4 == 0 and a 16-byte aligned destination (checked by the callers); rows < nrows.
-#ifndef DRPO_DEFER_SAVES
-#define DRPO_DEFER_SAVES 1   // A/B macro
-#endif
 template <int NT, int ROWS>
 __device__ __forceinline__ void save_tile_lds(const float* t, int ldt, float* gy, int N, int nrows) {
   const int n4 = N >> 2;
@@ -360,7 +330,7 @@ __device__ __forceinline__ void save_tile_lds(const float* t, int ldt, float* gy
 
 // a layer save the caller may defer to save_tile_lds: post-activation only, 4-aligned width
 __device__ __forceinline__ bool save_deferrable(const float* gy, const float* gz, int N) {
-  return DRPO_DEFER_SAVES && gy && !gz && N > 16 && (N & 3) == 0 && (((uintptr_t)gy) & 15) == 0;
+  return gy && !gz && N > 16 && (N & 3) == 0 && (((uintptr_t)gy) & 15) == 0;
 }
 
 template <int NW, int RB, int MAXC, int ACT>
@@ -379,13 +349,13 @@ __device__ __forceinline__ void dense_epilogue(const f32x4 (&acc)[RB][MAXC], con
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + swz_row<2>(r, g);
-        const float z = swz_pick<2>(acc[rb][c], r, g) + bv;
+        const int row = rb * 16 + 4 * g + r;
+        const float z = acc[rb][c][r] + bv;
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
         if (col < N && row < gs.nrows) {
-          if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-          if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -640,7 +610,7 @@ __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const 
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[q * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc, r, g);
+  for (int r = 0; r < 4; ++r) red[q * 256 + (4 * g + r) * 16 + l15] = acc[r];
   return 0.f;
 }
 
@@ -731,7 +701,7 @@ __device__ __forceinline__ void tile_dense_narrow_partials(const float* in, int 
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
   lds_barrier();
 }
 
@@ -782,7 +752,7 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
   lds_barrier();
   for (int e = tid; e < RB * 256; e += NW * 64) {
     const int rb = e >> 8, rr = (e >> 4) & 15, col = e & 15;
@@ -794,8 +764,8 @@ __device__ __forceinline__ void tile_dense_narrow(const float* in, int ldi, int 
     const int row = rb * 16 + rr;
     if (out) out[row * ldo + col] = (col < N) ? y : 0.f;
     if (col < N && row < gs.nrows) {
-      if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-      if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+      if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+      if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
     }
   }
 }
@@ -881,13 +851,13 @@ __device__ __forceinline__ void tile_dense_pair_core(const float* in, int ldi, i
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + swz_row<2>(r, g);
-        const float z = swz_pick<2>(acc[rb][c], r, g) + bvs[c];
+        const int row = rb * 16 + 4 * g + r;
+        const float z = acc[rb][c][r] + bvs[c];
         const float y = act_fn<ACT>(z);
         out[row * ldo + col] = (col < nn) ? y : 0.f;
         if (col < nn && row < gs.nrows) {
-          if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-          if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -1001,13 +971,13 @@ __device__ __forceinline__ void tile_dense_pair2_core(const float* in1, const fl
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * g + swz_row<2>(r, g);
-        const float z = swz_pick<2>(acc[rb][c], r, g) + bvs[c];
+        const int row = rb * 16 + 4 * g + r;
+        const float z = acc[rb][c][r] + bvs[c];
         const float y = act_fn<ACT>(z);
         if (out) out[row * ldo + col] = (col < nn) ? y : 0.f;
         if (col < nn && row < gs.nrows) {
-          if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-          if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+          if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+          if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
         }
       }
   }
@@ -1170,7 +1140,7 @@ __device__ __forceinline__ void tile_dense_narrow_pair_partials(const float* in1
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
   lds_barrier();
 }
 
@@ -1220,7 +1190,7 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(acc[rb], r, g);
+    for (int r = 0; r < 4; ++r) red[(wave * RB + rb) * 256 + (4 * g + r) * 16 + l15] = acc[rb][r];
   lds_barrier();
   for (int e = tid; e < 2 * RB * 256; e += NW * 64) {
     const int which = e / (RB * 256), e2 = e - which * RB * 256;
@@ -1236,8 +1206,8 @@ __device__ __forceinline__ void tile_dense_narrow_pair(const float* in1, const f
     out[row * ldo + col] = (col < nn) ? y : 0.f;
     const GSave& gs = which ? gs2 : gs1;
     if (col < nn && row < gs.nrows) {
-      if (!DRPO_PROBE_NOSAVE && gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
-      if (!DRPO_PROBE_NOSAVE && gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
+      if (gs.gy) gstore(gs.gy + (size_t)row * gs.ldg + col, y);
+      if (gs.gz) gstore(gs.gz + (size_t)row * gs.ldg + col, z);
     }
   }
 }

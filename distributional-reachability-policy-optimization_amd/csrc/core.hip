@@ -24,12 +24,10 @@ DRPO_API int drpo_version(void) { return 1; }
 // individual kernels on the stream they run on. The events are timing-only: created
 // without the system-scope release a default event record carries (measured: a
 // default timing event left the GPU idle ~5.7 us per record between two kernels,
-// profiles/r04a), since nothing reads memory through them. DRPO_EVENT_SYSTEM_FENCE=1
-// restores the default (A/B).
+// profiles/r04a), since nothing reads memory through them.
 DRPO_API int drpo_event_create(void** ev) {
   hipEvent_t e;
-  static const bool sys_fence = getenv("DRPO_EVENT_SYSTEM_FENCE") != nullptr;
-  hipError_t r = sys_fence ? hipEventCreate(&e) : hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   if (r != hipSuccess) {
     drpo_set_error("hipEventCreate: %s", hipGetErrorString(r));
     return DRPO_EHIP;

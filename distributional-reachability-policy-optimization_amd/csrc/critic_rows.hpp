@@ -12,17 +12,11 @@ namespace drpo {
 // chain per workgroup (profiles/sac_stamps.py); the hardware forms (v_exp_f32 /
 // v_log_f32 / v_rcp_f32, ~1 ulp) cut it, at ~1e-6 relative error -- far inside the SAC
 // parity tolerances. log1p of a small argument uses its series (log(1 + y) alone loses
-// the low bits of y). DRPO_CRITIC_FAST_MATH=0: the libm forms (A/B).
-#ifndef DRPO_CRITIC_FAST_MATH
-#define DRPO_CRITIC_FAST_MATH 1
-#endif
-__device__ __forceinline__ float cr_exp(float x) { return DRPO_CRITIC_FAST_MATH ? fast_exp(x) : expf(x); }
-__device__ __forceinline__ float cr_log(float x) {
-  return DRPO_CRITIC_FAST_MATH ? 0.69314718055994531f * __builtin_amdgcn_logf(x) : logf(x);
-}
-__device__ __forceinline__ float cr_rcp(float x) { return DRPO_CRITIC_FAST_MATH ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
+// the low bits of y).
+__device__ __forceinline__ float cr_exp(float x) { return fast_exp(x); }
+__device__ __forceinline__ float cr_log(float x) { return 0.69314718055994531f * __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float cr_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float cr_softplus(float x) {   // torch softplus (beta 1, threshold 20)
-  if (!DRPO_CRITIC_FAST_MATH) return softplusf(x);
   if (x > 20.f) return x;
   const float y = fast_exp(-fabsf(x));
   const float l1p = y < 1e-3f ? y * (1.f - 0.5f * y) : 0.69314718055994531f * __builtin_amdgcn_logf(1.f + y);

@@ -113,13 +113,7 @@ __device__ __forceinline__ void ff_epi_bwd(const f32x4 (&acc)[1][MAXC], int N, f
 // epilogue and barrier, so the cold first touch of a layer's weights (the mirrors were
 // rewritten by the previous step's Adam) overlaps that epilogue instead of stalling the
 // layer's first MFMA; the ring then streams the rest of the layer as tile_dense_mma does.
-#ifndef DRPO_FIT_PF
-#define DRPO_FIT_PF 6   // ring depth of the trunk-width (2 blocks per wave) layers
-#endif
-#ifndef DRPO_FIT_DEFER
-#define DRPO_FIT_DEFER 0   // A/B macro (measured no gain, profiles/r05/fit_defer): coalesced saves after each barrier
-#endif
-constexpr int FPT = DRPO_FIT_PF;
+constexpr int FPT = 6;   // ring depth of the trunk-width (2 blocks per wave) layers
 constexpr int FPH = 4;   // ring depth of the heads phase (3-4 blocks per wave)
 static_assert(FPT >= 5, "the first layer (K <= 64) is preloaded whole");
 
@@ -324,14 +318,9 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   lds_barrier();
   FSTAMP(1);
 
-  // Saves for the weight gradients (layer inputs y, every dZ): with DRPO_FIT_DEFER the
-  // epilogues write LDS only and the whole workgroup stores the tile after the phase's
-  // barrier as 16-byte stores (save_tile_lds: a 200-float row in 50 lanes) instead of
-  // the accumulator layout's row-strided 4-byte stores.
-  auto dsave = [&](const float* buf, float* gy) {
-    if (DRPO_FIT_DEFER && gy) save_tile_lds<FF_NT, FF_ROWS>(buf, FF_LDH, gy, Hm, nrows);
-  };
-  auto esave = [&](float* gy) { return DRPO_FIT_DEFER ? nullptr : gy; };   // the epilogue's share
+  // Saves for the weight gradients (layer inputs y, every dZ) leave from the epilogues.
+  // (Deferring them to 16-byte stores of the LDS tile after each barrier measured no
+  // gain: profiles/r05/fit_defer.)
   // ---- trunk ------------------------------------------------------------------------
   float* sy0 = tsave && t0.sy ? t0.sy + zr * Hm : nullptr;
   float* sy1 = tsave && t1.sy ? t1.sy + zr * Hm : nullptr;
@@ -348,11 +337,10 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
     ff_pre2<NK>(t1.W + (size_t)z * t1.wstride, NCB, bqt);
     ff_bias2(t1.b + (size_t)z * t1.bstride, Hm, bvt);
     FSTAMP(11);
-    ff_epi_fwd(acc, bv, Hm, T1, Z1, esave(sy0), Hm, nrows);
+    ff_epi_fwd(acc, bv, Hm, T1, Z1, sy0, Hm, nrows);
     FSTAMP(12);
   }
   lds_barrier();
-  dsave(T1, sy0);
   FSTAMP(2);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool second = wave >= FF_NW / 2;
@@ -367,10 +355,9 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
     ff_mma2<NK>(T1, t1.W + (size_t)z * t1.wstride, NCB, bqt, acc);
     ff_pre_heads<NK>(base, NCB, l0.W + (size_t)z * l0.wstride, l0.b + (size_t)z * l0.bstride, Hm,
                      l1.W + (size_t)z * l1.wstride, bqh, nbh, bvh);
-    ff_epi_fwd(acc, bvt, Hm, T2, Z2, esave(sy1), Hm, nrows);
+    ff_epi_fwd(acc, bvt, Hm, T2, Z2, sy1, Hm, nrows);
   }
   lds_barrier();
-  dsave(T2, sy1);
   FSTAMP(3);
   // ---- both heads: hidden + output layers, one phase ----------------------------------
   auto& Hb = Bd.net[1 + h];
@@ -385,13 +372,12 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
     const float* P = l0.W + (size_t)z * l0.wstride;
     float* out = second ? HB : HA;
     float* zb = own ? ZH : nullptr;
-    float* gy = own ? esave(syh) : nullptr;
+    float* gy = own ? syh : nullptr;
     const float* Pb1 = o1.W + (size_t)z * o1.wstride;
     if (nc == 4) ff_heads_core<4, NK>(base, T2, P, Hm, bqh, nbh, bvh, out, zb, gy, nrows, slot, Pb1, bqt);
     else ff_heads_core<3, NK>(base, T2, P, Hm, bqh, nbh, bvh, out, zb, gy, nrows, slot, Pb1, bqt);
   }
   lds_barrier();
-  dsave(h == 0 ? HA : HB, syh);
   FSTAMP(4);
   // ---- NLL (drpo_ens_loss's arithmetic; ens_upstream in csrc/mlp.hip) -------------------
   float* Gd = T1;   // head h's output gradient (T1, the trunk's first layer y, is dead)
@@ -466,29 +452,23 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
     FSTAMP(13);
     ff_pre2<NK>(o0.W + (size_t)z * o0.wstride, NCB, bqt);
     FSTAMP(14);
-    ff_epi_bwd(acc, Hm, HB, ZH, esave(dzh), Hm, nrows);
+    ff_epi_bwd(acc, Hm, HB, ZH, dzh, Hm, nrows);
     FSTAMP(15);
   }
   lds_barrier();
-  dsave(HB, dzh);
   FSTAMP(6);
   {
     f32x4 acc[1][2];
     ff_mma2<NK>(HB, o0.W + (size_t)z * o0.wstride, NCB, bqt, acc);
     ff_pre2<NK>(tb.W + (size_t)z * tb.wstride, NCB, bqt);
-    ff_epi_bwd(acc, Hm, HA, Z2, esave(dzt2), Hm, nrows);
+    ff_epi_bwd(acc, Hm, HA, Z2, dzt2, Hm, nrows);
   }
   lds_barrier();
-  dsave(HA, dzt2);
   FSTAMP(7);
   {
     f32x4 acc[1][2];
     ff_mma2<NK>(HA, tb.W + (size_t)z * tb.wstride, NCB, bqt, acc);
-    ff_epi_bwd(acc, Hm, DRPO_FIT_DEFER ? T1 : nullptr, Z1, esave(dzt1), Hm, nrows);
-  }
-  if (DRPO_FIT_DEFER) {
-    lds_barrier();
-    dsave(T1, dzt1);
+    ff_epi_bwd(acc, Hm, nullptr, Z1, dzt1, Hm, nrows);
   }
   FSTAMP(8);
 }
@@ -497,15 +477,8 @@ __global__ __launch_bounds__(FF_NT) void fit_fb_kernel(FitFbArgs args) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   FitK& k = *(FitK*)__builtin_amdgcn_kernarg_segment_ptr();
   (void)args;
-#ifndef DRPO_FIT_REPS
-#define DRPO_FIT_REPS 1   // probe builds only: the body run R times (its last run's stamps kept)
-#endif
-#pragma nounroll
-  for (int rep = 0; rep < DRPO_FIT_REPS; ++rep) {
-    if (k.f.net[0].L[1].dout == 200) fit_fb_body<13>(k, smem);
-    else fit_fb_body<16>(k, smem);
-    if (DRPO_FIT_REPS > 1) __syncthreads();
-  }
+  if (k.f.net[0].L[1].dout == 200) fit_fb_body<13>(k, smem);
+  else fit_fb_body<16>(k, smem);
 }
 
 static_assert(sizeof(FitFbArgs) <= 4096, "fused fit kernarg");

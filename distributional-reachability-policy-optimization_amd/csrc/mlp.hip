@@ -11,7 +11,6 @@
 //                   trunk), saving dZ_l for the weight gradients and the input
 //                   gradient (e.g. dQ/da for the actor update).
 // (the weight gradients dW = dZ^T Y of every layer run in csrc/wgrad.hip)
-#include <stdlib.h>
 
 #include "common.hpp"
 #include "critic_rows.hpp"
@@ -30,15 +29,6 @@ constexpr int MAXL = 3;
 constexpr int MAXN = 3;
 
 }  // namespace
-
-// A/B macro of the multi-job forward (profiles/r05/fwd_ab): the policy head one thread
-// per (row, action dim) on the hardware transcendentals (squash_head_tile: 44.9 vs
-// 45.6 us per forward launch, SAC 66.3 vs 65.6 TFLOP/s). (Measured and removed: the
-// first layer's fragments loaded during the input staging, 48.0 vs 45.6 us: the
-// staging's input loads then wait behind the fragments in the in-order vmcnt.)
-#ifndef DRPO_FWD_HEAD_TILE
-#define DRPO_FWD_HEAD_TILE 1
-#endif
 
 
 // ---------------------------------------------------------------------------
@@ -81,15 +71,6 @@ DRPO_API int drpo_debug_stamps_clear() {
 #define STAMPW(i) \
   do {            \
   } while (0)
-#endif
-#ifndef DRPO_DEFER_NET
-#define DRPO_DEFER_NET 1    // deferred saves (save_tile_lds) in run_net_g / heads_pair / pair_nets
-#endif
-#ifndef DRPO_DEFER_HEADS
-#define DRPO_DEFER_HEADS 0   // on: 60 VGPRs spilled in mlp_fwd_multi_kernel<1> (the paired heads layer)
-#endif
-#ifndef DRPO_DEFER_PAIR
-#define DRPO_DEFER_PAIR 0   // on: the paired nets (a.f1) 2 us slower (profiles/r05/defer_saves)
 #endif
 template <int ACT, int RB>
 __device__ __forceinline__ void run_layer_act(const float* in, int ldi, const drpo_mlp_layer_t& L, const float* W,
@@ -248,7 +229,7 @@ __device__ __forceinline__ float* run_net_g(const drpo_mlp_net_t& __restrict__ n
     float* out = (cur == bufA) ? bufB : bufA;
     const drpo_mlp_layer_t& L = n.L[l];
     const GSave gs = layer_save(L, z, rows, row0, nrows);
-    const bool defer = DRPO_DEFER_NET && save_deferrable(gs.gy, gs.gz, L.dout);
+    const bool defer = save_deferrable(gs.gy, gs.gz, L.dout);
     run_layer<RB>(cur, LDH, L, z, rows, row0, nrows, out, red, !defer);
     lds_barrier();
     if (defer) save_tile_lds<FW_NT, 16 * RB>(out, LDH, gs.gy, L.dout, nrows);
@@ -279,18 +260,13 @@ __device__ __forceinline__ void heads_pair_act(const drpo_mlp_fwd_t* __restrict_
   const drpo_mlp_layer_t& B0 = a->net[2].L[0];
   const drpo_mlp_layer_t& A1 = a->net[1].L[1];
   const drpo_mlp_layer_t& B1 = a->net[2].L[1];
-  // (the save pointers formed again after the barrier: held across the paired layer
-  // they cost it 64 spilled VGPRs)
-  const bool dA = DRPO_DEFER_HEADS && save_deferrable(A0.sy, A0.sz, A0.dout),
-             dB = DRPO_DEFER_HEADS && save_deferrable(B0.sy, B0.sz, B0.dout);
-  const GSave none{nullptr, nullptr, 0, 0};
+  // (saves from the epilogue: deferring them to 16-byte stores after the barrier, as
+  // run_net_g does, spilled 60 VGPRs in this paired layer, profiles/r05/defer_saves)
   tile_dense_pair<FW_NW, RB, 4, ACT0, 16, 2>(T, LDH, 256, A0.W + (size_t)z * A0.wstride, A0.b + (size_t)z * A0.bstride,
                                           A0.dout, hA, B0.W + (size_t)z * B0.wstride, B0.b + (size_t)z * B0.bstride,
-                                          B0.dout, hB, LDH, dA ? none : layer_save(A0, z, a->rows, row0, nrows),
-                                          dB ? none : layer_save(B0, z, a->rows, row0, nrows));
+                                          B0.dout, hB, LDH, layer_save(A0, z, a->rows, row0, nrows),
+                                          layer_save(B0, z, a->rows, row0, nrows));
   lds_barrier();
-  if (dA) save_tile_lds<FW_NT, 16 * RB>(hA, LDH, layer_save(A0, z, a->rows, row0, nrows).gy, A0.dout, nrows);
-  if (dB) save_tile_lds<FW_NT, 16 * RB>(hB, LDH, layer_save(B0, z, a->rows, row0, nrows).gy, B0.dout, nrows);
   STAMP(5);
   tile_dense_narrow_pair<FW_NW, RB, ACT1>(hA, hB, LDH, A0.dout, A1.W + (size_t)z * A1.wstride,
                                           A1.b + (size_t)z * A1.bstride, A1.dout, o, B1.W + (size_t)z * B1.wstride,
@@ -324,7 +300,7 @@ __device__ __forceinline__ void heads_pair(const drpo_mlp_fwd_t* __restrict__ a,
 // The fused squashed-Gaussian head of a policy job (squashed_gaussian_row's arithmetic,
 // src/policy.py:88-97, src/squashed_gaussian.py): one thread per (row, action dim)
 // instead of one per row, on the hardware transcendentals of critic_rows.hpp
-// (DRPO_CRITIC_FAST_MATH; ~1e-6 relative), log(std) taken as the log-std itself (the
+// (~1e-6 relative), log(std) taken as the log-std itself (the
 // reference's log(exp(log_std))); the per-dim log-prob terms are summed per row in
 // dimension order through LDS (lpt). The per-row libm chain it replaces was 5.6-8 k
 // cycles at the end of every policy workgroup (profiles/r05/sac_fwd_stamps).
@@ -342,11 +318,11 @@ __device__ __forceinline__ void squash_head_tile(const float* outp, int row0, in
       const float mu = rrow[d];
       const float ls = -6.f + 10.f * cr_rcp(1.f + cr_exp(-rrow[A + d]));
       const float sd = cr_exp(ls) * 1.0f;
-      if (hd.amean) gstore(hd.amean + k, DRPO_CRITIC_FAST_MATH ? fast_tanh(mu) : tanhf(mu));
+      if (hd.amean) gstore(hd.amean + k, fast_tanh(mu));
       if (mode != 2) {
         const float e = normal_at(hd.eps, k, seed, ctr, hd.site);
         const float u = (mode == 0) ? e * sd + mu : mu + e * sd;
-        const float act = DRPO_CRITIC_FAST_MATH ? fast_tanh(u) : tanhf(u);
+        const float act = fast_tanh(u);
         if (hd.a) gstore(hd.a + k, act);
         if (a_lds) a_lds[r * LDH + d] = act;   // chain: the action as the next net's input columns
         if (hd.u) gstore(hd.u + k, u);
@@ -386,35 +362,16 @@ __device__ __forceinline__ void pair_nets_nk(const drpo_mlp_net_t& A, const drpo
   auto W = [&](const drpo_mlp_layer_t& L) { return L.W + (size_t)z * L.wstride; };
   auto bb = [&](const drpo_mlp_layer_t& L) { return L.b + (size_t)z * L.bstride; };
   const drpo_mlp_layer_t &L0 = N.L[0], &L1 = N.L[1];
-  // deferred saves (save_tile_lds) only when both nets' layers defer: the whole
-  // workgroup stores both tiles after the barrier
-  const GSave none{nullptr, nullptr, 0, 0};
-  bool d;
-  {
-    const GSave s = layer_save(L0, z, rows, row0, nrows);
-    d = DRPO_DEFER_PAIR && save_deferrable(A.L[0].sy, A.L[0].sz, A.L[0].dout) &&
-        save_deferrable(B.L[0].sy, B.L[0].sz, B.L[0].dout);
-    tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, NK0, 0, 2>(in, LDH, L0.din, W(L0), bb(L0), L0.dout, second ? bB : bA,
-                                                           LDH, d ? none : s, nullptr, wl);
-  }
+  // (saves from the epilogue: deferred 16-byte saves measured 2 us slower here,
+  // profiles/r05/defer_saves)
+  tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, NK0, 0, 2>(in, LDH, L0.din, W(L0), bb(L0), L0.dout, second ? bB : bA,
+                                                         LDH, layer_save(L0, z, rows, row0, nrows), nullptr, wl);
   lds_barrier();
-  if (d) {
-    save_tile_lds<FW_NT, 16 * RB>(bA, LDH, layer_save(A.L[0], z, rows, row0, nrows).gy, A.L[0].dout, nrows);
-    save_tile_lds<FW_NT, 16 * RB>(bB, LDH, layer_save(B.L[0], z, rows, row0, nrows).gy, B.L[0].dout, nrows);
-  }
   STAMP(2);
-  {
-    const GSave s = layer_save(L1, z, rows, row0, nrows);
-    d = DRPO_DEFER_PAIR && save_deferrable(A.L[1].sy, A.L[1].sz, A.L[1].dout) &&
-        save_deferrable(B.L[1].sy, B.L[1].sz, B.L[1].dout);
-    tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, 16, 0, 2>(second ? bB : bA, LDH, 256, W(L1), bb(L1), L1.dout,
-                                                          second ? T : in, LDH, d ? none : s, nullptr, wl);
-  }
+  tile_dense_core<FW_NW / 2, RB, 4, ACT_RELU, 16, 0, 2>(second ? bB : bA, LDH, 256, W(L1), bb(L1), L1.dout,
+                                                        second ? T : in, LDH, layer_save(L1, z, rows, row0, nrows),
+                                                        nullptr, wl);
   lds_barrier();
-  if (d) {
-    save_tile_lds<FW_NT, 16 * RB>(in, LDH, layer_save(A.L[1], z, rows, row0, nrows).gy, A.L[1].dout, nrows);
-    save_tile_lds<FW_NT, 16 * RB>(T, LDH, layer_save(B.L[1], z, rows, row0, nrows).gy, B.L[1].dout, nrows);
-  }
   STAMP(3);
   const drpo_mlp_layer_t &A2 = A.L[2], &B2 = B.L[2];
   tile_dense_narrow_pair<FW_NW, RB, ACT_NONE>(in, T, LDH, A2.din, W(A2), bb(A2), A2.dout, bA, W(B2), bb(B2), B2.dout,
@@ -559,13 +516,7 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   // job, on net 1's (head2; its log-prob scratch after head's)
   const drpo_policy_head_t& hd = a->head;
   if (hd.mode != 0 && outp && net == 0) {
-    if (DRPO_FWD_HEAD_TILE) {
-      squash_head_tile<ROWS>(outp, row0, nrows, hd, m.seed, m.ctr, red);
-    } else if (tid < nrows) {
-      const float* rrow = outp + tid * LDH;
-      squashed_gaussian_row([&](int c) { return rrow[c]; }, (int64_t)(row0 + tid), hd.A, hd.mode - 1, hd.eps, m.seed,
-                            m.ctr, hd.site, hd.a, hd.logp, hd.u, hd.e, hd.amean);
-    }
+    squash_head_tile<ROWS>(outp, row0, nrows, hd, m.seed, m.ctr, red);
   }
   if (outp2 && a->head2.mode != 0) squash_head_tile<ROWS>(outp2, row0, nrows, a->head2, m.seed, m.ctr, red + ROWS * 8);
   STAMP(15);
@@ -647,13 +598,9 @@ DRPO_API int drpo_mlp_forward_multi(const drpo_mlp_fwd_t* jobs_host, const drpo_
   }
   if (tiles == 0) return DRPO_OK;
   // 32-row tiles halve the weight bytes per MFMA but allow only one 8-wave workgroup
-  // per CU (LDS); measured slower at B=4096 (profiles/r01), so only for launches
-  // with >= 8 workgroups per CU at 16-row tiles
-  static const int force_rb = [] {
-    const char* e = getenv("DRPO_FWD_RB");
-    return e ? atoi(e) : 0;
-  }();
-  if (force_rb == 2 || (force_rb != 1 && tiles * slots * nbatch >= 2048)) {
+  // per CU (LDS); measured slower at B=4096 (profiles/r01, profiles/r04/bench_stats), so
+  // only for launches with >= 8 workgroups per CU at 16-row tiles
+  if (tiles * slots * nbatch >= 2048) {
     const size_t lds = sizeof(float) * ((size_t)4 * 2 * FW_ROWS * LDH + FW_NW * 2 * 256);
     mlp_fwd_multi_kernel<2><<<dim3((unsigned)((tiles + 1) / 2), slots, nbatch), FW_NT, lds, stream>>>(m);
   } else {

@@ -16,7 +16,6 @@
 // rollout needs no host synchronisation.
 #include <stdarg.h>
 #include <stdio.h>
-#include <stdlib.h>
 
 #define DRPO_UNIFORM_WEIGHT_LOADS 1   // scalar-base weight loads (see load_pk)
 #ifndef DRPO_PF_SCALE
@@ -424,22 +423,14 @@ __device__ __forceinline__ const float* step_opaque(const float* ptr) {
   return ptr;
 }
 
-// A/B knobs of the persistent kernel (profiles/gpu_ab_persist.sh):
-//  DRPO_PERSIST_KARG  read the per-step pointers / sizes through an opaque kernarg
-//                     pointer at their point of use (scalar loads) instead of holding
-//                     the whole argument block in SGPRs across the loop (SGPR spills)
-//  DRPO_PREFETCH_M1   issue the elite member's first-layer fragments and biases at the
-//                     top of the step, so they arrive while the actor runs
-//  DRPO_ABIAS_LDS     actor biases staged in LDS once per launch (LW variant)
-#ifndef DRPO_PERSIST_KARG
-#define DRPO_PERSIST_KARG 1   // config 2: 248 -> 242 us per launch (profiles/r03/ab_persist)
-#endif
-#ifndef DRPO_PREFETCH_M1
-#define DRPO_PREFETCH_M1 1   // member L1 weights fetched at the top of the step (profiles/r05/rollout_ab: +0.7-1.3 %)
-#endif
-#ifndef DRPO_ABIAS_LDS
-#define DRPO_ABIAS_LDS 0
-#endif
+// Two choices of the persistent kernel, each measured (A/B, one box):
+//  - the per-step pointers / sizes are read through an opaque kernarg pointer at their
+//    point of use (PARG: scalar loads) instead of holding the whole argument block in
+//    SGPRs across the loop (SGPR spills): config 2 248 -> 242 us per launch
+//    (profiles/r03/ab_persist);
+//  - the elite member's first-layer fragments and biases are issued at the top of the
+//    step, so they arrive while the actor runs: +0.7-1.3 % (profiles/r05/rollout_ab).
+// (Actor biases staged in LDS once per launch measured no gain: profiles/r05/rollout_ab.)
 
 struct PersistArgs {
   int S, A, C, Ha, Hm, B, H, ntiles;
@@ -475,14 +466,10 @@ __device__ __forceinline__ PersistArgsK persist_args() {
   asm volatile("" : "+s"(q));
   return q;
 }
-#if DRPO_PERSIST_KARG
 #define PARG(f) (persist_args()->f)
-#else
-#define PARG(f) (p.f)
-#endif
 
 // First layer with K <= 16 (one k-step) whose fragments / biases were loaded ahead
-// (DRPO_PREFETCH_M1): the wave's MAXC blocks, clamped to the last valid block (its
+// (top of the step): the wave's MAXC blocks, clamped to the last valid block (its
 // duplicate results are discarded by the epilogue).
 template <int NW, int MAXC>
 struct Layer1Frags {
@@ -591,8 +578,8 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float y = act_fn<ACT_SILU>(swz_pick<2>(acc[rb][c], r, g) + bvs[c]);
-        out[(rb * 16 + 4 * g + swz_row<2>(r, g)) * ldo + col] = col < N ? y : 0.f;
+        const float y = act_fn<ACT_SILU>(acc[rb][c][r] + bvs[c]);
+        out[(rb * 16 + 4 * g + r) * ldo + col] = col < N ? y : 0.f;
       }
   }
   wave_lds_sync();
@@ -610,7 +597,7 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red_slot[rb * 256 + (4 * g + swz_row<1>(r, g)) * 16 + l15] = swz_pick<1>(pacc[rb], r, g);
+    for (int r = 0; r < 4; ++r) red_slot[rb * 256 + (4 * g + r) * 16 + l15] = pacc[rb][r];
 }
 
 template <int NW, int RB, int NC, int NK>
@@ -687,14 +674,12 @@ __device__ __forceinline__ void persist_noise(const float* eps_a, const float* e
 // each step, and the layers run at the CU's L2 read rate). Needs S <= 16,
 // Ha == 256, 2A <= 16 and the LDS to spare (host check).
 constexpr int PERSIST_L2_LDS = 3;
-#ifndef DRPO_M2_SPLIT
-#define DRPO_M2_SPLIT 1   // A/B macro: the member hidden layer split over K for SIMD balance
-#endif
 
 // PM: the dynamics heads' path fixed at compile time (1: paired heads, S+1 <= 16 and
-// Hm = 200; 0: the general path; -1: chosen at run time), so a specialised kernel holds
-// registers for one path only
-template <int RB, int NW, bool LW, int PM = -1>
+// Hm = 200; 0: the general path), so each kernel holds registers for one path only
+// (spilled VGPRs 53 -> 33 / 1 -> 0 against one kernel with a run-time path choice,
+// profiles/r03/pm_ab)
+template <int RB, int NW, bool LW, int PM>
 __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p) {
   constexpr int ROWS = RB * 16;
   constexpr int NT = NW * 64;
@@ -732,15 +717,14 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
   float* wl1 = vecs + 256;                  /* LW: actor L1 mirror [16 cb][256] */               \
   float* wl3 = wl1 + 16 * 256;              /* LW: actor head mirror [16 k-steps][256] */        \
   float* wl2 = wl3 + 16 * 256;              /* LW: actor L2 [16 cb][PERSIST_L2_LDS][256] */      \
-  float* abl = wl2 + 16 * PERSIST_L2_LDS * 256;   /* LW + DRPO_ABIAS_LDS: ab1 | ab2 | ab3 */      \
-  (void)wl1; (void)wl2; (void)wl3; (void)abl;                                                 \
+  (void)wl1; (void)wl2; (void)wl3;                                                            \
   (void)h3; (void)dout; (void)lout; (void)act; (void)rew; (void)nz_a; (void)nz_m;    \
   (void)flags; (void)alive; (void)s_nalive; (void)red; (void)v_nm; (void)v_ns; (void)v_lo; (void)v_hi;
   const int tile = blockIdx.x;
   const int row0 = tile * ROWS;
   const int nrows = min(ROWS, B - row0);
   const int Ha = p.Ha, Hm = p.Hm;
-  const bool paired = PM >= 0 ? PM == 1 : (S1 <= 16 && Hm == 200);
+  constexpr bool paired = PM == 1;
   {
   PERSIST_LDS_LAYOUT(0, p.ldx, p.ldh, p.ldm, p.lds)
   if (tid < 256) {
@@ -763,13 +747,6 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     for (int e = tid; e < 16 * PERSIST_L2_LDS * 64; e += NT) {
       const int cb = e / (PERSIST_L2_LDS * 64), r = e - cb * PERSIST_L2_LDS * 64;
       reinterpret_cast<f32x4*>(wl2)[e] = gload(a2 + cb * 16 * 64 + r);
-    }
-    if constexpr (DRPO_ABIAS_LDS) {
-      for (int e = tid; e < 256; e += NT) {
-        abl[e] = gload(p.ab1 + e);
-        abl[256 + e] = gload(p.ab2 + e);
-      }
-      if (tid < 2 * A) abl[512 + tid] = gload(p.ab3 + tid);
     }
   }
 
@@ -801,11 +778,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     // the elite member's slices, formed where they are used (PARG: re-read per use)
 #define MW(f, st) (PARG(f) + (size_t)m * PARG(st))
 #define MB(f, n) (PARG(f) + (size_t)m * (n))
-#if DRPO_PREFETCH_M1
     Layer1Frags<NW, MAXC> m1;
     const bool m1_pre = S + A <= 16;
     if (m1_pre) layer1_prefetch<NW, MAXC>(MW(mW1, ms_in), MB(mb1, Hm), Hm, m1);
-#endif
 
     if (t == 2) RSTAMP(0);
     if (t == 2) RSTAMP(1);
@@ -816,11 +791,11 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     // ---- actor MLP (src/policy.py:61-100) ------------------------------------
     if constexpr (LW) {
       tile_dense_impl<NW, RB, MAXC, ACT_RELU, 1, 1>(xin, ldx, S, step_opaque(PARG(aW1)),
-                                                   DRPO_ABIAS_LDS ? abl : step_opaque(PARG(ab1)), Ha, h1, ldh,
+                                                   step_opaque(PARG(ab1)), Ha, h1, ldh,
                                                    GSave{nullptr, nullptr, 0, 0}, wl1);
       lds_barrier();
       if (t == 2) RSTAMP(2);
-      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 16, PERSIST_L2_LDS>(h1, ldh, Ha, aW2, DRPO_ABIAS_LDS ? abl + 256 : ab2,
+      tile_dense_impl<NW, RB, MAXC, ACT_RELU, 16, PERSIST_L2_LDS>(h1, ldh, Ha, aW2, ab2,
                                                                  Ha, h2, ldh, GSave{nullptr, nullptr, 0, 0}, wl2);
     } else {
       tile_dense<NW, RB, MAXC, ACT_RELU>(xin, ldx, S, step_opaque(PARG(aW1)), step_opaque(PARG(ab1)), Ha, h1, ldh);
@@ -843,14 +818,9 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
       float bmu = 0.f, braw = 0.f;
       if (tid < ROWS * A) {   // ROWS * A <= NT (A <= 8)
         const int d = tid % A;
-        if constexpr (LW && DRPO_ABIAS_LDS) {
-          bmu = abl[512 + d];
-          braw = abl[512 + A + d];
-        } else {
-          const float* ab3 = step_opaque(PARG(ab3));
-          bmu = gload(ab3 + d);
-          braw = gload(ab3 + A + d);
-        }
+        const float* ab3 = step_opaque(PARG(ab3));
+        bmu = gload(ab3 + d);
+        braw = gload(ab3 + A + d);
       }
       tile_dense_narrow_partials<NW, RB, LW>(h2, ldh, Ha, step_opaque(PARG(aW3)), red, wl3);
       if (tid < ROWS * A) {
@@ -871,21 +841,18 @@ __global__ __launch_bounds__(NW * 64) void rollout_persist_kernel(PersistArgs p)
     if (t == 2) RSTAMP(4);
 
     // ---- elite member forward (src/dynamics.py:112-122) -----------------------
-#if DRPO_PREFETCH_M1
     if (m1_pre) layer1_run<NW, RB, MAXC, ACT_SILU>(xin, ldx, m1, Hm, h1, ldh);
     else
-#endif
     tile_dense<NW, RB, MAXC, ACT_SILU>(xin, ldx, S + A, MW(mW1, ms_in), MB(mb1, Hm), Hm, h1, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(5);
-#if DRPO_M2_SPLIT
     if (RB == 1 && NW == 8 && Hm == 200) {
-      // member hidden layer balanced over the SIMDs (13th block split over K)
+      // member hidden layer balanced over the SIMDs (13th block split over K;
+      // profiles/r04/m2_split)
       const float b12 = tile_dense_13s<ACT_SILU>(h1, ldh, MW(mW2, ms_hid), MB(mb2, Hm), h2, ldh, red);
       lds_barrier();
       tile_dense_13s_finish<ACT_SILU>(red, b12, h2, ldh);
     } else
-#endif
     tile_dense<NW, RB, MAXC, ACT_SILU>(h1, ldh, Hm, MW(mW2, ms_hid), MB(mb2, Hm), Hm, h2, ldh);
     lds_barrier();
     if (t == 2) RSTAMP(6);
@@ -1320,46 +1287,29 @@ static int rollout_fused(const drpo_rollout_desc_t* d, int rpt, int64_t rlen, hi
   a.lds = round_up(S, 4);
   for (int t = 0; t < H; ++t) a.members[t] = d->members[t];
 
-  static const int NW = [] {
-    const char* e = getenv("DRPO_ROLLOUT_NW");
-    return (e && atoi(e) == 16) ? 16 : 8;
-  }();
-  const int nw = rpt == 32 ? 8 : NW;
-  const size_t lds_bytes = persist_lds_bytes(S, A, d->Ha, d->Hm, rpt, nw);
+  // 8-wave workgroups (16 waves measured 3.5 % slower at config 2, profiles/r02/rollout_ab)
+  const size_t lds_bytes = persist_lds_bytes(S, A, d->Ha, d->Hm, rpt, 8);
   DRPO_REQUIRE(lds_bytes <= 160 * 1024, "drpo_rollout: LDS %zu too large", lds_bytes);
   // LDS-resident actor weights (see rollout_persist_kernel) when they fit
-  const size_t lw_bytes = sizeof(float) * ((size_t)(32 + 16 * PERSIST_L2_LDS) * 256 + (DRPO_ABIAS_LDS ? 528 : 0));
-  const bool lw = rpt == 16 && NW == 8 && S <= 16 && d->Ha == 256 && 2 * A <= 16 && lds_bytes + lw_bytes <= 160 * 1024 &&
-                  !getenv("DRPO_ROLLOUT_NO_LDS_WEIGHTS");
+  const size_t lw_bytes = sizeof(float) * (size_t)(32 + 16 * PERSIST_L2_LDS) * 256;
+  const bool lw = rpt == 16 && S <= 16 && d->Ha == 256 && 2 * A <= 16 && lds_bytes + lw_bytes <= 160 * 1024;
   const bool paired = S1 <= 16 && d->Hm == 200;   // the kernel's PM specialisation
-  static const bool pm_rt = getenv("DRPO_ROLLOUT_PM_RUNTIME") != nullptr;   // A/B: unspecialised kernels
-  static const bool scan_emit = getenv("DRPO_ROLLOUT_SCAN_EMIT") != nullptr;   // A/B: the two-launch tail
-  const bool self_emit = (int64_t)H * a.ntiles <= EMIT_SELF_MAX && !scan_emit;
+  const bool self_emit = (int64_t)H * a.ntiles <= EMIT_SELF_MAX;
   if (self_emit) {
     a.vptr_in = d->vptr;
     a.base_slot = off + H + 1;
   }
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[0], stream);
-  if (rpt == 32)
-  {
-    if (pm_rt)
-      rollout_persist_kernel<2, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
-    else if (paired)
-      rollout_persist_kernel<2, 8, false, 1><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
-    else
-      rollout_persist_kernel<2, 8, false, 0><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+  if (rpt == 32) {
+    if (paired) rollout_persist_kernel<2, 8, false, 1><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+    else rollout_persist_kernel<2, 8, false, 0><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+  } else if (lw) {
+    if (paired) rollout_persist_kernel<1, 8, true, 1><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
+    else rollout_persist_kernel<1, 8, true, 0><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
+  } else {
+    if (paired) rollout_persist_kernel<1, 8, false, 1><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
+    else rollout_persist_kernel<1, 8, false, 0><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   }
-  else if (NW == 16)
-    rollout_persist_kernel<1, 16, false><<<a.ntiles, 16 * 64, lds_bytes, stream>>>(a);
-  else if (lw)
-  {
-    if (paired && !pm_rt)
-      rollout_persist_kernel<1, 8, true, 1><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
-    else
-      rollout_persist_kernel<1, 8, true><<<a.ntiles, 8 * 64, lds_bytes + lw_bytes, stream>>>(a);
-  }
-  else
-    rollout_persist_kernel<1, 8, false><<<a.ntiles, 8 * 64, lds_bytes, stream>>>(a);
   DRPO_LAUNCH_CHECK("rollout_persist");
   if (d->step_events) hipEventRecord((hipEvent_t)d->step_events[1], stream);
   const dim3 eg((unsigned)((a.ntiles * rpt + 255) / 256), (unsigned)H);
@@ -1416,9 +1366,8 @@ DRPO_API int drpo_rollout(const drpo_rollout_desc_t* d, drpo_stream_t stream_) {
   RolloutWs w = rollout_ws(d->B, d->S, d->H, (char*)d->workspace);
   // 32-row tiles halve the weight bytes per MFMA once the batch fills the chip with
   // them (B >= 8192), when the wider tile still fits the LDS (not for tracking's S=51)
-  static const bool force16 = getenv("DRPO_ROLLOUT_RPT16") != nullptr;   // A/B
   const int rpt = d->rows_per_tile ? d->rows_per_tile
-                                   : (!force16 && d->B >= 256 * 32 &&
+                                   : (d->B >= 256 * 32 &&
                                               persist_lds_bytes(d->S, d->A, d->Ha, d->Hm, 32, 8) <= 160 * 1024
                                           ? 32 : 16);
   DRPO_REQUIRE(rpt == 16 || rpt == 32, "drpo_rollout: rows_per_tile must be 16 or 32");

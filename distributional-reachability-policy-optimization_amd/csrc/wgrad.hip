@@ -40,9 +40,12 @@
 //   - the last arriver learns it from the add's returned value and reads the slabs with
 //     `global_load ... sc1` (bypassing the per-CU L1, which is never refreshed by
 //     other CUs' stores), issued only after the add returned.
-// The __ATOMIC_ACQ_REL form of the ticket (DRPO_WGRAD_ACQREL=1, an A/B build) lowers to
-// `buffer_wbl2 sc1` + `buffer_inv sc1` around the add: a write-back of the XCD's whole L2
-// and an L1 invalidate, each ~1.7 us per workgroup (MI355X_MICROARCH.md, price list).
+// This is the first row of MI355X_MICROARCH.md's table of hand-offs measured with sc1
+// loads in place of the acquire (one lane per storing workgroup adds to one counter after
+// every wave's vmcnt(0) wait; the last adder, told by the returned value, loads with sc1).
+// An __ATOMIC_ACQ_REL ticket would lower to `buffer_wbl2 sc1` + `buffer_inv sc1` around
+// the add: a write-back of the XCD's whole L2 and an L1 invalidate, each ~1.7 us per
+// workgroup (the guide's price list) -- measured and rejected (profiles/r05/wgrad_setup).
 #include "common.hpp"
 #include "ens_reduce.hpp"
 
@@ -51,19 +54,7 @@ using namespace drpo;
 namespace {
 constexpr int WG_NW = 4;                 // waves per workgroup
 constexpr int WG_NT = WG_NW * 64;
-#ifndef DRPO_WG_D
-#define DRPO_WG_D 3
-#endif
-constexpr int WG_D = DRPO_WG_D;          // register ring slots (k-groups of 4 rows each; A/B macro)
-#ifndef DRPO_WGRAD_EARLY
-#define DRPO_WGRAD_EARLY 1               // A/B macro: single-chunk tiles load their finish operands early
-#endif
-#ifndef DRPO_WGRAD_PTT
-#define DRPO_WGRAD_PTT 1                 // A/B macro: the float4 finish's transposed refresh through LDS
-#endif
-#ifndef DRPO_WGRAD_ACQREL
-#define DRPO_WGRAD_ACQREL 0              // A/B macro: acq_rel ticket (see the memory-model note)
-#endif
+constexpr int WG_D = 3;                  // register ring slots (k-groups of 4 rows each; 3 measured best, profiles/r04/wgrad)
 constexpr int WG_ROWQ = 64;              // chunk granularity (rows)
 constexpr int WG_MAXITEMS = 16;
 constexpr int WG_SLD = 264;              // LDS slab stride per accumulator block (== 8 mod 32)
@@ -390,7 +381,7 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
       bvv = a.adam.v[eb + o0 + tid];
     }
   };
-  if (DRPO_WGRAD_EARLY && P.nch == 1) load_grad();
+  if (P.nch == 1) load_grad();
   // the 4 waves' partial tiles -> LDS slabs (conflict-free: lanes write consecutive words)
   float* R = lds;
 #pragma unroll
@@ -446,8 +437,7 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
     if (tid == 0) {
       unsigned* c = a.ctr + P.first_tile + tile_local;
       // relaxed: see the memory-model note at the top (gfx950 ordering, not C++ acq_rel)
-      const unsigned old = __hip_atomic_fetch_add(c, 1u, DRPO_WGRAD_ACQREL ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == (unsigned)(P.nch - 1);
       if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = last;
@@ -482,8 +472,6 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
         }
       }
     }
-  } else if (!DRPO_WGRAD_EARLY) {
-    load_grad();
   }
   if (adam) {
     // the finished gradient g = current terms + this launch's sum -> Adam (the
@@ -520,15 +508,10 @@ __device__ __forceinline__ void wgrad_unit(WgradArgsK& a, int q, int64_t u, floa
         if (PM)   // i .. i+3 are the 4 components of one lane of fragment (o>>4, i>>4)
           *reinterpret_cast<f32x4*>(PM + mb + ((int64_t)((o >> 4) * nks + (i >> 4)) << 8) +
                                     ((((i >> 2) & 3) * 16 + (o & 15)) << 2)) = p4;
-        if (PTM && !DRPO_WGRAD_PTT)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            PTM[mb + ((int64_t)((i >> 4) * ncb + (o >> 4)) << 8) + (((((o >> 2) & 3) * 16 + ((i + c) & 15))) << 2) +
-                (o & 3)] = p4[c];
 #pragma unroll
         for (int c = 0; c < 4; ++c) ap[4 * j + c] = p4[c];   // the new parameters (the transposed refresh)
       }
-      if (PTM && DRPO_WGRAD_PTT) {
+      if (PTM) {
         // transposed mirror: a float4 there is 4 consecutive outputs of one input, so the
         // tile goes through LDS ([64][65] floats over the partial-tile slabs) and each
         // thread stores 4 such float4s instead of 16 scattered floats
@@ -666,18 +649,10 @@ __global__ __launch_bounds__(WG_NT, 2) void mlp_wgrad_kernel(WgradArgs args) {
   for (int i = 1; i < WG_MAXITEMS; ++i) q += bid >= a.first[i] ? 1 : 0;
   const auto& P = a.pl[q];
   const int64_t u = bid - P.first_unit;
-#ifndef DRPO_WGRAD_REPS
-#define DRPO_WGRAD_REPS 1   // timing probes only: the unit run R times (results then wrong)
-#endif
-#pragma nounroll
-  for (int rep = 0; rep < DRPO_WGRAD_REPS; ++rep) {
-    if (DRPO_WGRAD_REPS > 1) STAMPG(0);
-    if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
-    else if (P.to == 64) wgrad_unit_v<64, 16>(a, q, u, wsm);
-    else if (P.ti == 64) wgrad_unit_v<16, 64>(a, q, u, wsm);
-    else wgrad_unit_v<16, 16>(a, q, u, wsm);
-    if (DRPO_WGRAD_REPS > 1) __syncthreads();
-  }
+  if (P.to == 64 && P.ti == 64) wgrad_unit_v<64, 64>(a, q, u, wsm);
+  else if (P.to == 64) wgrad_unit_v<64, 16>(a, q, u, wsm);
+  else if (P.ti == 64) wgrad_unit_v<16, 64>(a, q, u, wsm);
+  else wgrad_unit_v<16, 16>(a, q, u, wsm);
 }
 
 static_assert(sizeof(WgradArgs) <= 4096, "weight-gradient kernarg");
@@ -733,28 +708,14 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     ++m;
   }
   a.n = m;
-  static const bool vf_env = [] {   // A/B knob: the float4 finish (WgradPlan.vf)
-    const char* e = getenv("DRPO_WGRAD_VF");
-    return !(e && e[0] == '0');
-  }();
-  // chunk sizes: every unit about the same cost, all units resident at once (<= 2 per CU)
-  static const int per_cu = [] {   // A/B knob (profiles/wgrad_probe.py)
-    const char* e = getenv("DRPO_WGRAD_PER_CU");
-    const int v = e ? atoi(e) : 2;
-    return v >= 1 && v <= 64 ? v : 2;
-  }();
-  const int64_t slots = per_cu * (int64_t)wg_cus();
-  static const double min_rows = [] {   // A/B knob: minimum rows per unit (profiles/wgrad_probe.py)
-    const char* e = getenv("DRPO_WGRAD_MIN_ROWS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? (double)v : 0.0;
-  }();
+  // chunk sizes: every unit about the same cost, all units resident at once (2 per CU;
+  // 1, 3 or 4 per CU and minimum row counts per unit measured slower, profiles/r04)
+  const int64_t slots = 2 * (int64_t)wg_cus();
   auto units_for = [&](double per, int* nch, int* chunk) {
     int64_t tot = 0;
     for (int k = 0; k < m; ++k) {
       const Shape& s = sh[k];
-      double rows_per = per * 16.0 / kg_cost(s.to, s.ti);   // rows whose cost per wave is `per`
-      if (rows_per < min_rows) rows_per = min_rows;              // a unit's fixed costs need work to amortise
+      const double rows_per = per * 16.0 / kg_cost(s.to, s.ti);   // rows whose cost per wave is `per`
       int64_t c = (int64_t)((double)s.rows / (rows_per > 1 ? rows_per : 1) + 0.5);
       c = c < 1 ? 1 : c;
       int64_t ck = (s.rows + c - 1) / c;
@@ -783,8 +744,7 @@ int plan(const drpo_wgrad_item_t* items, int n, const drpo_ens_reduce_t* red, Pl
     P.va = (I.dout & 3) == 0 && ((uintptr_t)I.dz & 15) == 0 && ((uintptr_t)I.dz2 & 15) == 0 && (I.zstride & 3) == 0;
     P.z2 = I.dz2 != nullptr;
     P.vb = (I.din & 3) == 0 && ((uintptr_t)I.y & 15) == 0 && (I.ystride & 3) == 0;
-    P.vf = s.to == 64 && s.ti == 64 && (I.din & 3) == 0 && ((uintptr_t)I.gW & 15) == 0 && (I.gwstride & 3) == 0 &&
-           vf_env;
+    P.vf = s.to == 64 && s.ti == 64 && (I.din & 3) == 0 && ((uintptr_t)I.gW & 15) == 0 && (I.gwstride & 3) == 0;
     P.first_unit = unit;
     P.first_tile = tile;
     P.slab_off = slab;

@@ -18,7 +18,6 @@ The per-step ``loss.item()`` of the reference is deferred: losses land in a devi
 array that is read once at the end of fit (same returned list of floats).
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -43,8 +42,6 @@ SPLIT_HEADS_MAX_TILES = 256
 
 
 def split_heads(n, Z):
-    if os.environ.get('DRPO_SPLIT_HEADS', '1') == '0':
-        return False
     return (n + 15) // 16 * Z <= SPLIT_HEADS_MAX_TILES
 
 
@@ -67,9 +64,8 @@ def ens_fb_shapes(nets, S, A):
     """The shapes drpo_ens_fit_fb takes (csrc/fit.hip: the fit step's forward, NLL and
     backward-data in one launch): trunk [S+A <= 64 -> H -> H], heads [H -> H -> S+1 <= 16],
     swish hidden layers, identity outputs, H = 200 | 256 (the reference default:
-    src/dynamics.py:59-61,85-86, hidden_dim=200, trunk_layers=2, head_hidden_layers=1).
-    DRPO_FIT_FB=0 keeps the two launches (A/B)."""
-    if os.environ.get('DRPO_FIT_FB', '1') == '0' or len(nets) != 3 or S + A > 64 or S + 1 > 16:
+    src/dynamics.py:59-61,85-86, hidden_dim=200, trunk_layers=2, head_hidden_layers=1)."""
+    if len(nets) != 3 or S + A > 64 or S + 1 > 16:
         return False
     sw = ACT_ID['swish']
     t = nets[0].layers
@@ -84,19 +80,18 @@ def ens_fb_shapes(nets, S, A):
     return True
 
 
-def split_heads_bwd(n, Z):
-    if os.environ.get('DRPO_SPLIT_BWD', '1') == '0':     # A/B knob: the paired backward
-        return False
-    return split_heads(n, Z)
-
-
 class EnsembleEngine:
     def __init__(self, model):
         self.m = model
         # single-process fit: Adam (+ mirror refresh) fused into the weight-gradient launch
-        # (drpo_mlp_wgrad_adam; bitwise the same step as drpo_optim_step). DRPO_FIT_FUSED_ADAM=0
-        # keeps the separate optimizer launch (A/B).
-        self.fused_adam = os.environ.get('DRPO_FIT_FUSED_ADAM', '1') != '0'
+        # (drpo_mlp_wgrad_adam; bitwise the same step as drpo_optim_step). The three switches
+        # below are the production dispatch; the bitwise / parity tests turn them off to run
+        # the launches each fusion replaced as their reference
+        # (tests/test_gpu_configs.py::test_fit_fused_adam_matches_separate_step,
+        # ::test_fit_fb_matches_two_launches).
+        self.fused_adam = True
+        self.split_bwd = True     # one backward workgroup per (row tile, head); False: paired heads
+        self.fit_fb_enabled = True   # forward + NLL + backward-data as one launch (drpo_ens_fit_fb)
         self.ws = {}
         self.wg_ws = {}
         self.noise = None
@@ -166,7 +161,7 @@ class EnsembleEngine:
                     net.sy[l] = self.buf(f'{tag}.sy{j}{l}', rows, dout)
                     net.sz[l] = self.buf(f'{tag}.sz{j}{l}', rows, dout) if act == ACT_ID['swish'] else None
                     net.dz[l] = self.buf(f'{tag}.dz{j}{l}', rows, dout)
-                    if j == 0 and split_heads_bwd(n, Z):
+                    if j == 0 and self.split_bwd and split:
                         net.dz2[l] = self.buf(f'{tag}.dzb{l}', rows, dout)
             save_x = self.buf(f'{tag}.x', rows, S + A)
         else:
@@ -290,7 +285,7 @@ class EnsembleEngine:
 
     def _backward_descs(self, nets, strides, save_x, gD, gL, b, Z):
         """Backward-data descriptor and the weight-gradient items: (desc, [(items, n)]).
-        Split heads (split_heads_bwd) leave the trunk dZ as two terms, which the trunk
+        Split heads (EnsembleEngine.split_bwd) leave the trunk dZ as two terms, which the trunk
         layers' items carry as dz + dz2."""
         split = nets[0].dz2[0] is not None
         d = fill_bwd(nets, [None, gD, gL], b, trunk=True, nbatch=Z, wstride=strides, split_heads=split)
@@ -421,7 +416,7 @@ class EnsembleEngine:
         bd.upstream = 3 if fused else 0   # DRPO_UPSTREAM_ENS
         # the reference default shapes at split-heads grids: forward + NLL + backward-data
         # as ONE launch per (row tile, head) (drpo_ens_fit_fb)
-        fb = fused and bool(bd.split_heads) and ens_fb_shapes(nets, S, A)
+        fb = self.fit_fb_enabled and fused and bool(bd.split_heads) and ens_fb_shapes(nets, S, A)
         self.fit_fb = fb
         up = EnsUpstream()
         up.D, up.LVR = nets[1].sy[-1].data_ptr(), nets[2].sy[-1].data_ptr()
@@ -450,6 +445,9 @@ class EnsembleEngine:
         # and steps the bounds, overlapped with the members' launch on the main stream.
         # The next step's backward (which reads the bounds and rewrites the partials)
         # waits for it.
+        # (a member shard and batch DP exclude each other: member_sharding() is None under
+        # dp_mode='batch', and no shard path sum-reduces the member gradients)
+        assert sh is None or getattr(m, 'dp_mode', 'auto') != 'batch'
         fuse_sh = self.fused_adam and fused and sh is not None and len(wl) == 1
         self.fit_path = 'fused' if fuse else ('fused-shard' if fuse_sh else 'separate')   # (tests, probes)
         if fuse or fuse_sh:

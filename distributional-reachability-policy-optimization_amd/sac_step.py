@@ -18,7 +18,6 @@ kernels (production) or the reference's recorded draws (parity TapeNoise), which
 are consumed here in the reference's call order.
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -71,15 +70,6 @@ class Net:
 
 def _p(t):
     return 0 if t is None else t.data_ptr()
-
-
-def _job_order(key, jobs):
-    """A/B knob: DRPO_SAC_REVERSE = comma-separated launch-key prefixes whose job lists
-    (= workgroup dispatch order) are reversed."""
-    rev = os.environ.get('DRPO_SAC_REVERSE', '')
-    if rev and any(key.startswith(p) for p in rev.split(',') if p):
-        return jobs[::-1]
-    return jobs
 
 
 def noise_tag(eps):
@@ -191,7 +181,7 @@ def with_head(d, mode, A, eps, site, a=None, logp=None, u=None, e=None, amean=No
     return d
 
 
-def wgrad_items(entries, rows, sq=None, key=None):
+def wgrad_items(entries, rows, sq=None):
     """entries: [(net, inputs_per_layer[, segment])] -> (ctypes array of WgradItem, count,
     {segment: partial slots used}). With sq = {segment: device tensor}, every item of a
     segment writes the sums of squares of its finished gradient tiles into consecutive
@@ -199,8 +189,6 @@ def wgrad_items(entries, rows, sq=None, key=None):
     L = _lib.lib()
     items, used = [], {}
     units = [(ent[0], ent[1], ent[2] if len(ent) > 2 else None, l) for ent in entries for l in range(len(ent[0].layers))]
-    if key is not None:
-        units = _job_order(key, units)   # A/B knob (item order = dispatch order)
     for net, ins, seg, l in units:
         W, b, din, dout, act, WT = net.layers[l]
         gW, gb = net.grad_layers[l]
@@ -317,6 +305,10 @@ class SACEngine:
         self.loss_pos = 0
         self._zeroed = set()   # groups whose grads the last fused step left zeroed
         self.noise = None
+        # production dispatch: the MLPMultiplier forward as a post chain of the bound's job
+        # (False: its own launch, the reference of
+        # tests/test_gpu_configs.py::test_multiplier_post_chain_matches_separate_launch)
+        self.post_mult = True
 
     # ------------------------------------------------------------------ buffers
     def buf(self, name, *shape, dtype=torch.float32):
@@ -448,7 +440,7 @@ class SACEngine:
         built once and kept in device memory."""
         d = self.desc.get(key)
         if d is None:
-            jobs = _job_order(key, builder())
+            jobs = builder()
             arr = (MlpFwd * len(jobs))(*jobs)
             d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(fwd_flops(j) for j in jobs))
         arr, dev, nj, fl = d
@@ -460,7 +452,7 @@ class SACEngine:
     def _run_bwd_multi(self, key, builder, head=None, actor=None):
         d = self.desc.get(key)
         if d is None:
-            jobs = _job_order(key, builder())
+            jobs = builder()
             arr = (MlpBwd * len(jobs))(*jobs)
             d = self.desc[key] = (arr, self._upload(arr), len(jobs), sum(bwd_flops(j) for j in jobs))
         arr, dev, nj, fl = d
@@ -552,9 +544,9 @@ class SACEngine:
 
     def _post_mult(self):
         """The multiplier forward as a post chain of the bound's job (csrc/mlp.hip,
-        drpo_mlp_fwd_t.post); DRPO_SAC_POST_MULT=0 keeps its own launch (A/B)."""
-        return (self._ccb_fused() and self.S + 1 <= 64 and self.nets['mult'].layers[0][2] == self.S + 1 and
-                os.environ.get('DRPO_SAC_POST_MULT', '1') != '0')
+        drpo_mlp_fwd_t.post) when the shapes allow it (self.post_mult)."""
+        return (self.post_mult and self._ccb_fused() and self.S + 1 <= 64 and
+                self.nets['mult'].layers[0][2] == self.S + 1)
 
     def _cc_bound_after(self, name, out, dist):
         """drpo_cc_head over the saved head outputs of job `name` when _ccb could not fuse it."""
@@ -652,10 +644,7 @@ class SACEngine:
         # the actor jobs, q pair, certificate, qt chain, cc_t chain (94.3 us; cc_t, qt, cc, q
         # 97.2; cc, q, cc_t, qt 100.4); with them, actor, certificate, q pair, cc_t, qt
         # (105.5 us; actor, q, cc, qt, cc_t 112.9; actor, chains, plain 111.4; chains, plain,
-        # actor 119.5). DRPO_SAC_EARLY_FIRST / _CF_PLAIN_FIRST / _CF_REVERSED /
-        # _CFA_REVERSED override (A/B).
-        early_first = early_actor and os.environ.get('DRPO_SAC_EARLY_FIRST', '1') == '1'
-        plain_first = os.environ.get('DRPO_SAC_CF_PLAIN_FIRST', '1' if early_actor else '0') == '1'
+        # actor 119.5).
 
         def cf_jobs():
             chains = [with_pre(fill_fwd(self._cc_nets('t'), [(s2c, S), (None, A), (None, 0)], B, trunk=True),
@@ -664,13 +653,9 @@ class SACEngine:
                                Net(n['actor'].layers), HEAD_SAMPLE, A, e1, SITE_PI_NEXT, logp=lp2)]
             plain = [fill_fwd(self._cc_nets(), [(self.bs, S), (self.ba, A), (None, 0)], B, trunk=True),
                      fill_fwd([n['q0'], n['q1']], [(self.bs, S), (self.ba, A), (None, 0)], B, save_x=xs, pair=pq)]
-            actor = self._actor_f1_jobs(None, None) if early_actor else []
-            main = plain + chains if plain_first else chains + plain
-            if not early_actor and os.environ.get('DRPO_SAC_CF_REVERSED', '1') == '1':
-                main = main[::-1]          # q pair, certificate, target chains
-            elif early_actor and os.environ.get('DRPO_SAC_CFA_REVERSED', '0') == '1':
-                main = plain[::-1] + chains[::-1]
-            return actor + main if early_first else main + actor
+            if early_actor:   # actor, certificate, q pair, cc_t chain, qt chain
+                return self._actor_f1_jobs(None, None) + plain + chains
+            return plain[::-1] + chains[::-1]          # q pair, certificate, qt chain, cc_t chain
         self._run_multi('c.f' + rk + noise_tag(e1) + ('+a' if early_actor else ''), cf_jobs, ctr)
         loss = self._loss_slots(2)
         self._clean_grads(sol.critic_group)
@@ -713,7 +698,7 @@ class SACEngine:
         if dist:
             items.append((n['cc_ls'], [tsy[-1], n['cc_ls'].sy[0]], 'cc'))
         sq = self._sq('c', ('c', 'cc'))
-        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq, key='c.wg'),
+        used = self._run_wgrad('c.wg' + str(int(dist)) + ('f' if sq else ''), lambda: wgrad_items(items, B, sq),
                                sums=[(lpart[:2 * nt], loss[0]), (lpart[2 * nt:], loss[1])])
         cg = sol.critic_group
         self.dp.sum_(cg.grad)      # the 1/G of the mean rides in the optimizer segments
@@ -895,8 +880,8 @@ class SACEngine:
     def _early_actor(self, noise):
         """The actor update's first forward joins the critic update's forward launch:
         production (Philox) noise only -- a recorded tape hands over the actor's draws
-        after the critic's -- and DRPO_SAC_EARLY_ACTOR=0 keeps the separate 'a.f1' launch."""
-        return not getattr(noise, 'parity', False) and os.environ.get('DRPO_SAC_EARLY_ACTOR', '1') != '0'
+        after the critic's."""
+        return not getattr(noise, 'parity', False)
 
     def _actor_f1_jobs(self, e5, e6):
         """The actor update's first forward (src/ssac.py:459-461,489-490): actor and safe

@@ -1,8 +1,7 @@
 """Micro-benchmark of drpo_mlp_wgrad (csrc/wgrad.hip) on the SAC critic update's item
 set at B rows (config 2: B = 4096) and on single items, timed with HIP events over
 back-to-back launches. With DRPO_LIB_OVERRIDE=<...>/libdrpo_hip_stamps.so it also
-prints the per-workgroup phase cycles (s_memtime stamps). A/B knob: the environment
-variable DRPO_WGRAD_PER_CU (resident workgroups per CU the planner sizes for).
+prints the per-workgroup phase cycles (s_memtime stamps).
 
 python profiles/wgrad_probe.py [rows]"""
 import ctypes
@@ -109,11 +108,10 @@ def stamps(items, rows):
 
 def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-    res = {'rows': rows, 'per_cu': os.environ.get('DRPO_WGRAD_PER_CU', '2')}
+    res = {'rows': rows}
     critic = make(CRITIC, rows)
     res['critic'] = time_launch(critic, rows)
     res['critic_stamps'] = stamps(critic, rows)
-    res['per_cu'] += '/min_rows=' + os.environ.get('DRPO_WGRAD_MIN_ROWS', '0')
     for name, shapes in (('actor', ACTOR), ('mult', MULT), ('256x256', [(256, 256)]), ('3x256x256', [(256, 256)] * 3),
                          ('256x16', [(256, SA)]), ('1x256', [(1, 256)])):
         it = make(shapes, rows)

@@ -251,11 +251,12 @@ def gen_constraints(out):
     np.savez_compressed(os.path.join(out, 'constraints.npz'), **d)
 
 
-def gen_rollout(out, name, seed):
-    cfg = small_config(name)
+def gen_rollout(out, name, seed, cfg=None, tag=None, keep=None):
+    """keep: state-dict key prefixes stored (None: all)."""
+    cfg = cfg or small_config(name)
     alg = build_alg(name, cfg, seed)
     d = meta(name, cfg, alg)
-    d.update(sd_dict(alg))
+    d.update({k: v for k, v in sd_dict(alg).items() if keep is None or k[3:].startswith(keep)})
     d.update(fill_replay(alg, name, 1200, seed + 1, alg.con_dim))
     states = alg.replay_buffer.get('states')
     alg.model_ensemble.state_normalizer.fit(states)
@@ -270,7 +271,7 @@ def gen_rollout(out, name, seed):
     d['out/n'] = np.array(n)
     for k, v in alg.virt_buffer.get(as_dict=True).items():
         d['out/' + k] = t2n(v)
-    np.savez_compressed(os.path.join(out, f'rollout_{name}.npz'), **d)
+    np.savez_compressed(os.path.join(out, f'rollout_{tag or name}.npz'), **d)
 
 
 def gen_ensemble(out, name, seed):
@@ -346,8 +347,16 @@ def solver_lrs(sol):
     return np.array([out['critic'], out['actor'], out['actor_safe'], out['multiplier']], dtype=np.float64)
 
 
-def gen_ssac(out, name, seed, tag, distributional, uncertainty, sac_extra=None):
-    cfg = small_config(name, distributional=distributional, uncertainty=uncertainty)
+def _changed(sd, prefixes):
+    """the snapshot entries of the groups an update step writes (fixture size)"""
+    return {k: v for k, v in sd.items() if prefixes is None or k[4:].startswith(prefixes)}
+
+
+def gen_ssac(out, name, seed, tag, distributional, uncertainty, sac_extra=None, cfg=None, snapshots=None):
+    """snapshots: per update, the state-dict prefixes stored after it (None: all keys);
+    the full-width fixture keeps the groups each update writes."""
+    cfg = cfg or small_config(name, distributional=distributional, uncertainty=uncertainty)
+    snap = snapshots or (None, None, None, None)
     if sac_extra:
         cfg.update({'sac_cfg': dict(sac_extra)})
     alg = build_alg(name, cfg, seed)
@@ -363,7 +372,7 @@ def gen_ssac(out, name, seed, tag, distributional, uncertainty, sac_extra=None):
         m.state_normalizer.fit(torch.from_numpy(synth_states(name, 500, rng)))
         m._elite_inds = [2, 0, 1]
         d['model/elite_inds'] = np.array(m._elite_inds)
-    d.update(sd_dict(sol, 'sd0/'))
+    d.update(_changed(sd_dict(sol, 'sd0/'), snap[0]))
     d['sd0/log_alpha'] = t2n(sol.log_alpha)
     batch = synth_batch(alg, name, cfg.sac_cfg.batch_size, rng)
     # the reference preprocesses in SMBPO.update_solver; feed preprocessed values directly
@@ -373,18 +382,18 @@ def gen_ssac(out, name, seed, tag, distributional, uncertainty, sac_extra=None):
         lq, lqc = sol.update_critic(*batch)
     d.update(tp.to_npz_dict('critic_tape'))
     d['out/lq'], d['out/lqc'] = t2n(lq), t2n(lqc)
-    d.update(sd_dict(sol, 'sd1/'))
+    d.update(_changed(sd_dict(sol, 'sd1/'), snap[1]))
     d['lr1'] = solver_lrs(sol)
     with Tape() as tp:
         sol.update_actor_and_alpha(batch[0])
     d.update(tp.to_npz_dict('actor_tape'))
-    d.update(sd_dict(sol, 'sd2/'))
+    d.update(_changed(sd_dict(sol, 'sd2/'), snap[2]))
     d['sd2/log_alpha'] = t2n(sol.log_alpha)
     d['lr2'] = solver_lrs(sol)
     with Tape() as tp:
         sol.update_multiplier(batch[0])
     d.update(tp.to_npz_dict('mult_tape'))
-    d.update(sd_dict(sol, 'sd3/'))
+    d.update(_changed(sd_dict(sol, 'sd3/'), snap[3]))
     d['lr3'] = solver_lrs(sol)
     np.savez_compressed(os.path.join(out, f'ssac_{tag}.npz'), **d)
 
@@ -418,6 +427,22 @@ def gen_cost(out):
     # two rollout_and_update() calls through the device batch path (violation flags
     # gathered from the buffers)
     gen_smbpo_update(out, 'point-robot', 46, 'cost_point', False, {'constrained_fcn': 'cost'})
+
+
+def gen_fullwidth(out):
+    """the reference's DEFAULT widths (actor / critics / certificate /
+    multiplier 256, model 200; SMBPO.Config / SSAC.Config defaults), so the 256- and
+    200-wide tiling paths meet a reference-held vector directly. SSAC: one update_critic
+    + update_actor_and_alpha + update_multiplier at B = 64 (DRPO flags); rollout: B = 64,
+    H = 2 at E = 7 / 5 elites. Only the groups each step writes are stored after it."""
+    sac_groups = ('actor.', 'actor_safe.', 'critic.', 'critic_target.', 'constraint_critic.',
+                  'constraint_critic_target.', 'multiplier.')
+    cfg = small_config('quadrotor', E=2, elites=2, model_hidden=200, hidden=256, sac_batch=64)
+    gen_ssac(out, 'quadrotor', 81, 'fullwidth_quad', True, True, cfg=cfg,
+             snapshots=(sac_groups, ('critic.', 'critic_target.', 'constraint_critic.', 'constraint_critic_target.'),
+                        ('actor.', 'actor_safe.'), ('multiplier.',)))
+    cfg = small_config('quadrotor', B=64, H=2, E=7, elites=5, model_hidden=200, hidden=256)
+    gen_rollout(out, 'quadrotor', 82, cfg=cfg, tag='fullwidth_quad', keep=('solver.actor.', 'model_ensemble.'))
 
 
 def gen_smbpo_update(out, name, seed, tag=None, distributional=True, sac_extra=None):
@@ -676,6 +701,9 @@ def main():
     if sys.argv[1:] == ['cost']:
         gen_cost(out)
         return
+    if sys.argv[1:] == ['fullwidth']:
+        gen_fullwidth(out)
+        return
     if sys.argv[1:] == ['robust']:
         gen_ssac(out, 'quadrotor', 34, 'robust_quad', False, True)
         gen_ssac(out, 'point-robot', 35, 'robust_point', False, True)
@@ -702,6 +730,7 @@ def main():
     gen_fit_epochs(out, 'quadrotor', 71, 17)
     gen_fit_epochs(out, 'tracking', 72, 18)
     gen_checkpoint(out, 61)
+    gen_fullwidth(out)
     print('golden fixtures written to', out)
 
 

@@ -442,8 +442,7 @@ def test_fit_fused_adam_matches_separate_step(c):
         g.mark_dirty()
         g.ensure_packed()
         eng.fused_adam = fused
-        import os
-        os.environ['DRPO_SPLIT_BWD'] = '1' if split else '0'
+        eng.split_bwd = split
         eng.ws.clear()
         eng.wg_ws.clear()
         losses = m.fit(alg.replay_buffer, steps=3, noise=DeviceNoise(1234))
@@ -457,8 +456,7 @@ def test_fit_fused_adam_matches_separate_step(c):
         l_s, o_s = run(False, True)
         l_p, o_p = run(False, False)
     finally:
-        import os
-        os.environ.pop('DRPO_SPLIT_BWD', None)
+        eng.split_bwd = True
         eng.fused_adam = True
     assert l_f == l_s
     for a, b, what in zip(o_f, o_s, ['data', 'm', 'v', 'packed', 'packedT', 'grad']):
@@ -479,7 +477,6 @@ def test_fit_fb_matches_two_launches(c):
     hidden columns instead of the separate forward's order, so D / log-var and everything
     downstream differ by summation order only: rtol 2e-5 on the saves, 1e-4 of each
     tensor's max-abs on the dZ."""
-    import os
     from drpo_amd.rng import DeviceNoise
     alg, cd = _alg(c, B=256)
     m = alg.model_ensemble
@@ -498,7 +495,7 @@ def test_fit_fb_matches_two_launches(c):
         m.optimizer.step_count = start[3]
         g.mark_dirty()
         g.ensure_packed()
-        os.environ['DRPO_FIT_FB'] = '1' if fb else '0'
+        eng.fit_fb_enabled = fb
         eng.ws.clear()
         eng.wg_ws.clear()
         losses = m.fit(alg.replay_buffer, steps=1, noise=DeviceNoise(4321))
@@ -510,7 +507,7 @@ def test_fit_fb_matches_two_launches(c):
         l_f, o_f = run(True)
         l_s, o_s = run(False)
     finally:
-        os.environ.pop('DRPO_FIT_FB', None)
+        eng.fit_fb_enabled = True
     np.testing.assert_allclose(l_f, l_s, rtol=2e-5)
     for k in names:
         a, b = o_f[k].cpu().numpy(), o_s[k].cpu().numpy()
@@ -525,16 +522,15 @@ def test_fit_fb_matches_two_launches(c):
 def test_multiplier_post_chain_matches_separate_launch(c):
     """The MLPMultiplier forward chained behind the constraint bound in the same
     workgroups (drpo_mlp_fwd_t.post: no 'a.mult' / 'm.mult' launch) against its own
-    launch (DRPO_SAC_POST_MULT=0), at the reference widths (256: the bound is formed
+    launch (SACEngine.post_mult = False), at the reference widths (256: the bound is formed
     in-kernel): the same layers on the same [s, bound] rows, so two actor and two
     multiplier updates leave bitwise the same parameters."""
-    import os
     from drpo_amd.rng import DeviceNoise
 
     def run(post):
-        os.environ['DRPO_SAC_POST_MULT'] = '1' if post else '0'
         alg, cd = _alg(c, B=1024)
         sol = alg.solver
+        sol.engine.post_mult = post
         assert sol.mlp_multiplier
         g = torch.Generator().manual_seed(5)
         noise = DeviceNoise(11)
@@ -546,10 +542,7 @@ def test_multiplier_post_chain_matches_separate_launch(c):
         assert sol.engine._ccb_fused() and sol.engine._post_mult() == post
         return {k: v.detach().clone() for k, v in sol.state_dict().items()}
 
-    try:
-        a = run(True)
-        b = run(False)
-    finally:
-        os.environ.pop('DRPO_SAC_POST_MULT', None)
+    a = run(True)
+    b = run(False)
     for k in a:
         assert torch.equal(a[k], b[k]), k

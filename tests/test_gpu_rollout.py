@@ -14,9 +14,12 @@ from oracle import drpo_oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('env', ['point-robot', 'quadrotor'])
-def test_rollout_matches_reference_fixture(env):
-    d = load_golden(f'rollout_{env}')
+@pytest.mark.parametrize('tag', ['point-robot', 'quadrotor', 'fullwidth_quad'])
+def test_rollout_matches_reference_fixture(tag):
+    """fullwidth_quad: the reference's default widths (actor 256, model 200, E = 7), B = 64,
+    H = 2: the production persist kernel's LDS-resident actor and paired-heads paths."""
+    d = load_golden(f'rollout_{tag}')
+    env = str(d['meta/env'])
     alg = small_smbpo(d, env)
     load_sd(alg, d, 'sd/')
     fill_replay(alg, d)
@@ -116,6 +119,31 @@ def original_row_tape(entries, ref, B):
             out.append((kind, v))
     assert off == len(dones)
     return out
+
+
+def test_fused_engine_matches_reference_fixture_full_width():
+    """The production fused-horizon engine (rollout_persist_kernel: LDS-resident actor,
+    member layer-1 prefetch, 13-block split, paired 200-wide heads) against the
+    reference-held full-width vector (rollout_fullwidth_quad: actor 256, model 200,
+    E = 7, B = 64, H = 2), the recorded draws re-indexed by original row."""
+    from drpo_amd import ops
+    d = load_golden('rollout_fullwidth_quad')
+    alg = small_smbpo(d, 'quadrotor')
+    load_sd(alg, d, 'sd/')
+    fill_replay(alg, d)
+    m = alg.model_ensemble
+    m.state_normalizer.mean.copy_(torch.from_numpy(d['model/norm_mean']))
+    m.state_normalizer.std.copy_(torch.from_numpy(d['model/norm_std']))
+    m._elite_inds = list(d['model/elite_inds'])
+    entries = drpo_amd.TapeNoise.from_npz(d, 'tape').entries
+    tape = drpo_amd.TapeNoise(original_row_tape(entries, {'dones': d['out/dones']}, alg.rollout_batch_size))
+    alg.rollout_engine = 2
+    out = ops.rollout(alg, alg.actor, None, tape, eps_layout=1)
+    torch.cuda.synchronize()
+    assert tape.done() and len(out) == int(d['out/n'])
+    got = alg.virt_buffer.get(as_dict=True)
+    for k in COMP:
+        close(got[k], d['out/' + k], tol=2e-4, msg=k)
 
 
 @pytest.mark.parametrize('env,B,H', FULL_WIDTH)

@@ -35,12 +35,14 @@ def check_params(module, ref, msg, skip=('model_ensemble', 'total_updates', 'log
 
 @pytest.mark.parametrize('tag', ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point',
                                  'scalar_mult_point', 'scalar_mult_quad', 'fixed_alpha_quad', 'log_alpha_point',
-                                 'cost_point', 'cost_quad'])
+                                 'cost_point', 'cost_quad', 'fullwidth_quad'])
 def test_ssac_updates_match_reference(tag):
     """scalar_mult..log_alpha are the SSAC configuration branches (scalar softplus
     multiplier with clamp(Qc) in the actor loss, autotune_alpha=False,
     use_log_alpha_loss=True); cost_* the constrained_fcn='cost' certificate (one-step
-    violation cost target from the actor's next action, no safe-actor update)."""
+    violation cost target from the actor's next action, no safe-actor update);
+    fullwidth_quad the reference's default widths (every net 256 wide: the production
+    pair / chain / paired-heads tilings), B = 64."""
     d = load_golden(f'ssac_{tag}')
     env = str(d['meta/env'])
     alg = small_smbpo(d, env)

@@ -117,9 +117,11 @@ def test_ensemble_fit_epochs(env):
         assert_same(P[k], v, msg=k)
 
 
-@pytest.mark.parametrize('env', ['point-robot', 'quadrotor'])
-def test_rollout(env):
-    d = load_golden(f'rollout_{env}')
+@pytest.mark.parametrize('tag', ['point-robot', 'quadrotor', 'fullwidth_quad'])
+def test_rollout(tag):
+    """fullwidth_quad: the reference's default widths (actor 256, model 200, E = 7)."""
+    d = load_golden(f'rollout_{tag}')
+    env = str(d['meta/env'])
     full = sd(d, 'sd/')
     P = {k[len('solver.'):]: v for k, v in full.items() if k.startswith('solver.actor.')}
     P.update({k: v for k, v in full.items() if k.startswith('model_ensemble.')})
@@ -151,7 +153,8 @@ def ssac_cfg(d):
 
 
 SSAC_TAGS = ['drpo_point', 'drpo_quad', 'vanilla_quad', 'robust_quad', 'robust_point', 'scalar_mult_point',
-             'scalar_mult_quad', 'fixed_alpha_quad', 'log_alpha_point', 'cost_point', 'cost_quad']
+             'scalar_mult_quad', 'fixed_alpha_quad', 'log_alpha_point', 'cost_point', 'cost_quad',
+             'fullwidth_quad']   # the reference's default widths (256): make_golden.gen_fullwidth
 
 
 @pytest.mark.parametrize('tag', SSAC_TAGS)
