@@ -45,6 +45,17 @@ void drpo_set_error(const char* fmt, ...);
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// sub-phase stamps of the layer cores: a profiling build's translation unit may define
+// CORE_STAMP before including this header (rollout.hip under DRPO_STAMPS)
+#ifndef CORE_STAMP
+#define CORE_STAMP(i) \
+  do {                \
+  } while (0)
+#define CORE_STAMP_W4(i) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace drpo {
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_TANH = 3 };
@@ -461,7 +472,7 @@ __device__ __forceinline__ void tile_dense_mma(const float* in, int ldi, const f
 
 // wv >= 0: the wave index within a sub-group of NW waves (a workgroup split into halves
 // that run different layers, e.g. pair_nets); RING > 0: the weight ring depth
-template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0, int RING = 0>
+template <int NW, int RB, int MAXC, int ACT, int NK, int NL = 0, int RING = 0, int STK = -1>
 __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K, const float* __restrict__ P,
                                                 const float* __restrict__ bias, int N, float* out, int ldo,
                                                 const GSave& gs, const float* Pl = nullptr, int wv = -1) {
@@ -526,6 +537,7 @@ __device__ __forceinline__ void tile_dense_core(const float* in, int ldi, int K,
           for (int rb = 0; rb < RB; ++rb)
             acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF][c][m], acc[rb][c], 0, 0, 0);
     }
+    if constexpr (STK >= 0) CORE_STAMP(STK);   // k-loop issued (profiling builds)
   } else {
     for (int kb = 0; kb < NKS; kb += PF_D) {
 #pragma unroll

@@ -17,10 +17,41 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <hip/hip_runtime.h>
+
 #define DRPO_UNIFORM_WEIGHT_LOADS 1   // scalar-base weight loads (see load_pk)
 #ifndef DRPO_PF_SCALE
 #define DRPO_PF_SCALE 12              // ring depth 6 for 2-block waves, 8 for 1-block waves
 #endif
+#ifdef DRPO_STAMPS
+// profiling builds only (profiles/stamps.py): per-workgroup s_memtime stamps
+__device__ unsigned long long g_stamps_roll[1 << 14][16];
+#define RSTAMP(i)                                                                                 \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long _t;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) g_stamps_roll[blockIdx.x][(i)] = _t;         \
+  } while (0)
+#define CORE_STAMP(i) RSTAMP(i)   // sub-phase stamps inside the layer cores (profiles/stamps.py)
+#define CORE_STAMP_W4(i)                                                                          \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long _t;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (threadIdx.x == 256 && blockIdx.x < (1u << 14)) g_stamps_roll[blockIdx.x][(i)] = _t;       \
+  } while (0)
+extern "C" __attribute__((visibility("default"))) int drpo_debug_stamps_rollout(unsigned long long* dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_roll), sizeof(unsigned long long) * 16 * (size_t)n);
+}
+#else
+#define RSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 #include "common.hpp"
 #include "env_constraints.hpp"
 
@@ -94,26 +125,6 @@ __device__ inline int64_t prp_index(uint64_t i, uint64_t N, int hb, const uint32
   }
   return (int64_t)(x % N);   // unreachable in practice (expected walk < 4)
 }
-
-#ifdef DRPO_STAMPS
-// profiling builds only (profiles/stamps.py): per-workgroup s_memtime stamps
-__device__ unsigned long long g_stamps_roll[1 << 14][16];
-#define RSTAMP(i)                                                                                 \
-  do {                                                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                                            \
-    unsigned long long _t;                                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
-    __builtin_amdgcn_sched_barrier(0);                                                            \
-    if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) g_stamps_roll[blockIdx.x][(i)] = _t;         \
-  } while (0)
-DRPO_API int drpo_debug_stamps_rollout(unsigned long long* dst, int n) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_roll), sizeof(unsigned long long) * 16 * (size_t)n);
-}
-#else
-#define RSTAMP(i) \
-  do {            \
-  } while (0)
-#endif
 
 template <int RB, int NW>
 __global__ __launch_bounds__(NW * 64) void rollout_step_kernel(RolloutStepArgs p) {
@@ -567,6 +578,8 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
         for (int rb = 0; rb < RB; ++rb)
           acc[rb][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[rb][m], bq[s % PF][c][m], acc[rb][c], 0, 0, 0);
   }
+  CORE_STAMP(13);
+  CORE_STAMP_W4(11);
   // the output layer's k-steps == this wave's hidden column blocks (K = N = Hm)
   f32x4 nb[NC];
 #pragma unroll
@@ -582,6 +595,8 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
         out[(rb * 16 + 4 * g + r) * ldo + col] = col < N ? y : 0.f;
       }
   }
+  CORE_STAMP_W4(12);
+  CORE_STAMP(14);
   wave_lds_sync();
   f32x4 pacc[RB];
 #pragma unroll
@@ -598,6 +613,7 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red_slot[rb * 256 + (4 * g + r) * 16 + l15] = pacc[rb][r];
+  CORE_STAMP(15);
 }
 
 template <int NW, int RB, int NC, int NK>
@@ -625,6 +641,7 @@ __device__ __forceinline__ void pair_split_heads(const float* in, int ldi, int N
   if (nc > 0)
     pair_split_nc<NW, RB, MAXC, NK>(nc, base, in, ldi, second ? P2 : P1, second ? b2 : b1, N, second ? out2 : out1,
                                     ldi, second ? Pn2 : Pn1, slot);
+
   else {   // a wave without blocks contributes zero partials
     const int lane = threadIdx.x & 63;
     for (int e = lane; e < RB * 256; e += 64) slot[e] = 0.f;

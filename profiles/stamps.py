@@ -99,7 +99,10 @@ def fused_stamps():
     c = int(os.environ.get('DRPO_STAMPS_CONFIG', '2'))   # BASELINE config (bench.CONFIGS)
     cd = bench.CONFIGS[c]
     env = cd['env']
-    alg = bench.make_alg(dev, cd['B'], min(cd['H'], 10), cd['E'], 0, bench.ENV_JSON[env],
+    # DRPO_STAMPS_H=3: the layer cores' sub-phase stamps (slots 11-15, written every
+    # step) then come from the same step t = 2 as the phase stamps
+    hz = min(cd['H'], int(os.environ.get('DRPO_STAMPS_H', '10')))
+    alg = bench.make_alg(dev, cd['B'], hz, cd['E'], 0, bench.ENV_JSON[env],
                          extra={'model_cfg': {'hidden_dim': hm}}, env=env)
     rep = bench.synth_replay(env, 100000, np.random.RandomState(0))
     alg.replay_buffer.extend(**{k: torch.from_numpy(v).to(dev) for k, v in rep.items()})
@@ -128,6 +131,11 @@ def fused_stamps():
         tot += d.mean()
         print(f'   {names[c]:12s} mean {d.mean():8.0f} min {d.min():8.0f} max {d.max():8.0f}')
     print(f'   total {tot:.0f} cycles')
+    if hz == 3 and (st[:, 11] > 0).all() and (st[:, 13] > 0).all():
+        m = lambda a, b: (st[:, b] - st[:, a]).mean()   # noqa: E731
+        print(f'   pair L1 wave 0 (4 blocks): k-loop issued {m(6, 13):.0f} | epilogue {m(13, 14):.0f} | '
+              f'output partials {m(14, 15):.0f} | barrier {m(15, 7):.0f}')
+        print(f'   pair L1 wave 4 (3 blocks, same SIMD): k-loop issued {m(6, 11):.0f} | epilogue {m(11, 12):.0f}')
     if env == 'tracking' and (st[:, 10] > 0).all():
         d = st[:, 10] - st[:, 7]
         print(f'   (of pair L2 + gauss: output layers {d.mean():.0f}, gauss {(st[:, 8] - st[:, 10]).mean():.0f})')
