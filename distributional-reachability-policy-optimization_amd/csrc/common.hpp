@@ -280,20 +280,19 @@ static __device__ __forceinline__ f32x4 load_pk(const float* __restrict__ P, int
 }
 
 // Weight fragments are streamed through a static register ring of depth PF_D:
-// the loads for k-step s+PF_D-1 are issued while k-step s computes, so up to
-// PF_D-1 k-steps (each >= 4*MAXC*RB MFMAs) of L2 latency are hidden even at one
-// wave per SIMD. The ring is indexed only by compile-time constants (unrolled),
-// so it stays in VGPRs.
-constexpr int PF_D = 4;
+// the loads for k-step s+PF_D-1 are issued while k-step s computes. The ring is
+// indexed only by compile-time constants (unrolled), so it stays in VGPRs.
+// Shallow rings: one k-step ahead is enough, and deeper rings only queue behind the
+// CU's L1 (round 6: rollout -1.5 %, SAC +0.3 % for 2 against 4-6 deep;
+// profiles/r06/ring_ab, and profiles/r06/feed_probe for the stand-alone k-loop).
+constexpr int PF_D = 2;
 
-// Ring depth of the unrolled (compile-time K) cores: deeper for waves that own few
-// column blocks (each k-step is then only 4*MAXC MFMAs of cover per wave)
-#ifndef DRPO_PF_SCALE
-#define DRPO_PF_SCALE 8
-#endif
+// Ring depth of the unrolled (compile-time K) cores: deeper for waves that own one
+// column block (each k-step is then only 4 MFMAs of cover per wave)
+constexpr int PF_SCALE = 4;
 template <int MAXC>
 __host__ __device__ constexpr int pf_depth() {
-  return DRPO_PF_SCALE / MAXC > PF_D ? (DRPO_PF_SCALE / MAXC > 8 ? 8 : DRPO_PF_SCALE / MAXC) : PF_D;
+  return PF_SCALE / MAXC > PF_D ? PF_SCALE / MAXC : PF_D;
 }
 
 // Optional global saves of the tile (rows < nrows only): gy = post-activation,
@@ -594,7 +593,8 @@ __device__ __forceinline__ void tile_dense_impl(const float* in, int ldi, int K,
 // issues 3.25 blocks of MFMAs instead of 4 on SIMD 0 and 3 on the others. Block 12's
 // partial tiles go to red[4][256]; after the caller's barrier tile_dense_13s_finish
 // sums them (fixed order), adds the bias and applies the activation. Returns the bias
-// value that thread (< 256) needs for the finish.
+// value that thread (< 256) needs for the finish. Weight ring 2 deep: deeper rings only
+// queue behind the L1 (6 / 8 deep: +3 % per rollout launch; profiles/r06/ring_ab).
 template <int ACT>
 __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const float* __restrict__ P,
                                                 const float* __restrict__ bias, float* out, int ldo, float* red) {
@@ -603,7 +603,7 @@ __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const 
   if (wave < 4) {
     const int col = 192 + (threadIdx.x & 15);
     const float b12 = col < 200 ? gload(bias + col) : 0.f;
-    tile_dense_core<8, 1, 2, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
+    tile_dense_core<8, 1, 2, ACT, 13, 0, 2>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
     return b12;
   }
   const int q = wave - 4;
@@ -611,7 +611,7 @@ __device__ __forceinline__ float tile_dense_13s(const float* in, int ldi, const 
   f32x4 bq[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) bq[u] = load_pk(P, 12, ks0 + (u < nks ? u : nks - 1), 13);
-  tile_dense_core<8, 1, 1, ACT, 13>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
+  tile_dense_core<8, 1, 1, ACT, 13, 0, 2>(in, ldi, 200, P, bias, 200, out, ldo, GSave{nullptr, nullptr, 0, 0});
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < 4; ++u) {

@@ -20,9 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #define DRPO_UNIFORM_WEIGHT_LOADS 1   // scalar-base weight loads (see load_pk)
-#ifndef DRPO_PF_SCALE
-#define DRPO_PF_SCALE 12              // ring depth 6 for 2-block waves, 8 for 1-block waves
-#endif
+
 #ifdef DRPO_STAMPS
 // profiling builds only (profiles/stamps.py): per-workgroup s_memtime stamps
 __device__ unsigned long long g_stamps_roll[1 << 14][16];
@@ -541,7 +539,9 @@ __device__ __forceinline__ void pair_split_core(int base, const float* in, int l
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[rb][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int PF = pf_depth<NC>();
+  // a 2-deep ring: deeper rings only queue behind the L1 (4: +0.6-0.9 %, 6: +3 %, 8: +5 %
+  // per launch; profiles/r06/ring_ab, profiles/r06/feed_probe)
+  constexpr int PF = 2;
   f32x4 bq[PF][NC];
 #pragma unroll
   for (int u = 0; u < PF - 1; ++u)

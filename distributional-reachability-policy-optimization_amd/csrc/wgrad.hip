@@ -850,6 +850,8 @@ static int wgrad_launch(const drpo_wgrad_item_t* items, int n, const drpo_ens_re
         if (mh->din[l] != I.din || mh->dout[l] != I.dout || rel < 0 || rel % per != 0) continue;
         const int64_t z0 = rel / per;
         if (z0 + I.nbatch > mh->nbatch[l] || (I.nbatch > 1 && I.gwstride != per)) continue;
+        DRPO_REQUIRE(p.a.pl[k].pk_layer < 0, "drpo_mlp_wgrad_adam: item %d matches layers %d and %d of the pack map", k,
+                     p.a.pl[k].pk_layer, l);
         p.a.pl[k].pk_layer = l;
         p.a.pl[k].pk_z0 = (int)z0;
       }

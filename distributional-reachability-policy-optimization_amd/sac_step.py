@@ -217,9 +217,9 @@ def wgrad_workspace(cache, key, arr, n, dev):
 
 def fwd_flops(d):
     """Algorithmic FLOPs of one drpo_mlp_forward launch (2 * rows * sum din*dout), the
-    chained policy of a multi-job launch included."""
+    chained policy and the post-chain multiplier of a multi-job launch included."""
     macs = 0
-    for n in [d.net[j] for j in range(d.nnets)] + [d.pre]:
+    for n in [d.net[j] for j in range(d.nnets)] + [d.pre, d.post]:
         for l in range(n.nl):
             macs += n.L[l].din * n.L[l].dout
     return 2 * d.rows * d.nbatch * macs
