@@ -113,25 +113,26 @@ __device__ __forceinline__ void ff_epi_bwd(const f32x4 (&acc)[1][MAXC], int N, f
 // epilogue and barrier, so the cold first touch of a layer's weights (the mirrors were
 // rewritten by the previous step's Adam) overlaps that epilogue instead of stalling the
 // layer's first MFMA; the ring then streams the rest of the layer as tile_dense_mma does.
-constexpr int FPT = 6;   // ring depth of the trunk-width (2 blocks per wave) layers
+constexpr int FPT = 3;   // ring depth of the trunk-width (2 blocks per wave) layers (6: +1 %,
+                         // profiles/r06/ring_ab2/fit)
 constexpr int FPH = 4;   // ring depth of the heads phase (3-4 blocks per wave)
-static_assert(FPT >= 5, "the first layer (K <= 64) is preloaded whole");
+constexpr int FP1 = 5;   // the first layer's ring: K <= 64 (4 k-steps) preloaded whole
 
 // Trunk-width layers: wave w owns column blocks w and w + 8 (clamped to a valid block:
 // a wave with one valid block computes a discarded copy of it, which costs nothing -- the
 // phase is bounded by SIMD 0's 4 blocks at N = 200, 2 per wave at N = 256)
-template <int NK>
-__device__ __forceinline__ void ff_pre2(const float* __restrict__ P, int NCB, f32x4 (&bq)[FPT][2]) {
+template <int NK, int R = FPT>
+__device__ __forceinline__ void ff_pre2(const float* __restrict__ P, int NCB, f32x4 (&bq)[R][2]) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-  for (int u = 0; u < FPT - 1; ++u)
+  for (int u = 0; u < R - 1; ++u)
     if (u < NK)
 #pragma unroll
       for (int c = 0; c < 2; ++c) bq[u][c] = load_pk(P, min(wave + FF_NW * c, NCB - 1), u, NK);
 }
 
-template <int NK>
-__device__ __forceinline__ void ff_mma2(const float* in, const float* __restrict__ P, int NCB, f32x4 (&bq)[FPT][2],
+template <int NK, int R = FPT>
+__device__ __forceinline__ void ff_mma2(const float* in, const float* __restrict__ P, int NCB, f32x4 (&bq)[R][2],
                                         f32x4 (&acc)[1][2]) {
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -141,9 +142,9 @@ __device__ __forceinline__ void ff_mma2(const float* in, const float* __restrict
   f32x4 an = *reinterpret_cast<const f32x4*>(in + l15 * FF_LDH + 4 * g), ac;
 #pragma unroll
   for (int s = 0; s < NK; ++s) {
-    if (s + FPT - 1 < NK) {
+    if (s + R - 1 < NK) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c) bq[(s + FPT - 1) % FPT][c] = load_pk(P, cbs[c], s + FPT - 1, NK);
+      for (int c = 0; c < 2; ++c) bq[(s + R - 1) % R][c] = load_pk(P, cbs[c], s + R - 1, NK);
     }
     ac = an;
     if (s + 1 < NK) an = *reinterpret_cast<const f32x4*>(in + l15 * FF_LDH + 16 * (s + 1) + 4 * g);
@@ -152,7 +153,7 @@ __device__ __forceinline__ void ff_mma2(const float* in, const float* __restrict
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int c = 0; c < 2; ++c)
-        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[m], bq[s % FPT][c][m], acc[0][c], 0, 0, 0);
+        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[m], bq[s % R][c][m], acc[0][c], 0, 0, 0);
   }
 }
 
@@ -274,15 +275,15 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
 
   // the first layer's whole weight tile, then the NLL's per-element inputs, ahead of
   // the input staging (independent loads: one round trip for all of them)
-  f32x4 bqt[FPT][2];
+  f32x4 bq1[FP1][2];
   float bvt[2];
   {
     const float* P = t0.W + (size_t)z * t0.wstride;
     switch (nk1) {
-      case 1: ff_pre2<1>(P, NCB, bqt); break;
-      case 2: ff_pre2<2>(P, NCB, bqt); break;
-      case 3: ff_pre2<3>(P, NCB, bqt); break;
-      default: ff_pre2<4>(P, NCB, bqt); break;
+      case 1: ff_pre2<1, FP1>(P, NCB, bq1); break;
+      case 2: ff_pre2<2, FP1>(P, NCB, bq1); break;
+      case 3: ff_pre2<3, FP1>(P, NCB, bq1); break;
+      default: ff_pre2<4, FP1>(P, NCB, bq1); break;
     }
     ff_bias2(t0.b + (size_t)z * t0.bstride, Hm, bvt);
   }
@@ -324,13 +325,14 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   // ---- trunk ------------------------------------------------------------------------
   float* sy0 = tsave && t0.sy ? t0.sy + zr * Hm : nullptr;
   float* sy1 = tsave && t1.sy ? t1.sy + zr * Hm : nullptr;
+  f32x4 bqt[FPT][2];
   {
     f32x4 acc[1][2];
     switch (nk1) {
-      case 1: ff_mma2<1>(xin, t0.W + (size_t)z * t0.wstride, NCB, bqt, acc); break;
-      case 2: ff_mma2<2>(xin, t0.W + (size_t)z * t0.wstride, NCB, bqt, acc); break;
-      case 3: ff_mma2<3>(xin, t0.W + (size_t)z * t0.wstride, NCB, bqt, acc); break;
-      default: ff_mma2<4>(xin, t0.W + (size_t)z * t0.wstride, NCB, bqt, acc); break;
+      case 1: ff_mma2<1, FP1>(xin, t0.W + (size_t)z * t0.wstride, NCB, bq1, acc); break;
+      case 2: ff_mma2<2, FP1>(xin, t0.W + (size_t)z * t0.wstride, NCB, bq1, acc); break;
+      case 3: ff_mma2<3, FP1>(xin, t0.W + (size_t)z * t0.wstride, NCB, bq1, acc); break;
+      default: ff_mma2<4, FP1>(xin, t0.W + (size_t)z * t0.wstride, NCB, bq1, acc); break;
     }
     FSTAMP(10);
     float bv[2] = {bvt[0], bvt[1]};
