@@ -1100,6 +1100,18 @@ __device__ __forceinline__ void tile_dense_catk(const float* in1, const float* i
   tile_dense_catk_nc<NW, RB, MAXC, ACT, NK>(nc, in1, in2, ldi, P1, P2, bias, N, out, ldo, gs);
 }
 
+// Which head (bit 2) and which base block (bits 0-1) a wave of an 8-wave workgroup runs in
+// the paired 200-wide heads (rollout.hip pair_split_heads, fit.hip's heads phase): the diff
+// head on waves 0, 1, 2, 7 (bases 0, 1, 2, 3), the log-var head on waves 3-6 (bases 0-3).
+// Base 0 owns 4 of the 13 blocks, so SIMD 0 (waves 0 / 4) and SIMD 3 (waves 3 / 7) carry 7
+// blocks each, the older wave the 4-block one on both. The round-5 map (head by wave half,
+// base w / 7 - w) had the 4-block wave older on SIMD 0 and younger on SIMD 3, and ran the
+// rollout 4.7 % and the fit 1.3 % slower at config 2 (profiles/r06/pair_map); making both
+// SIMDs alike either way (4-block wave older, or younger on both) measured the same.
+// The partial slot of (head, base) stays where narrow_pair_sum expects it:
+// head 0 slot base, head 1 slot NW/2 + 3 - base.
+__device__ __forceinline__ unsigned pair_wave_code(int wave) { return (0x37654210u >> (4 * wave)) & 7u; }
+
 // Partials-only form of tile_dense_narrow_pair (below): the value of layer `which`
 // at (row, col) is narrow_pair_sum<NW, RB>(red, which, row, col) + its bias, in the
 // same summation order as tile_dense_narrow_pair's epilogue.

@@ -5,8 +5,8 @@
 // backward it replaces (csrc/mlp.hip mlp_fwd_kernel + mlp_bwd_ens_kernel).
 //
 // A workgroup of head h keeps everything between the forward and the backward in LDS:
-//   x -> trunk L1 -> trunk L2 -> both heads' hidden layers (waves 0-3 the diff head,
-//   waves 4-7 the log-var head, each wave forming its split-K share of its head's
+//   x -> trunk L1 -> trunk L2 -> both heads' hidden layers (waves 0, 1, 2, 7 the diff
+//   head, waves 3-6 the log-var head: pair_wave_code), each wave forming its split-K share of its head's
 //   output layer from the columns it produced) -> D, log-var -> the NLL element
 //   gradients -> dZ of head h's output layer -> head h's hidden dZ -> its share of the
 //   trunk dZ (dz for h = 0, dz2 for h = 1; the trunk gradient is linear in the heads')
@@ -345,8 +345,9 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   lds_barrier();
   FSTAMP(2);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool second = wave >= FF_NW / 2;
-  const int base = second ? FF_NW - 1 - wave : wave;   // 7 / 6 / 6 / 7 blocks per SIMD
+  const unsigned pcode = pair_wave_code(wave);   // 7 / 6 / 6 / 7 blocks per SIMD (common.hpp)
+  const bool second = pcode >> 2;
+  const int base = pcode & 3;
   auto& Hn = F.net[second ? 2 : 1];
   auto& l0 = Hn.L[0];
   auto& l1 = Hn.L[1];
@@ -370,7 +371,7 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   {
     const bool own = (second ? 1 : 0) == h;
     const int nc = min(4, (NCB - base + 3) / 4);
-    float* slot = red + (size_t)wave * 256;
+    float* slot = red + (size_t)(second ? FF_NW / 2 + (FF_NW / 2 - 1 - base) : base) * 256;
     const float* P = l0.W + (size_t)z * l0.wstride;
     float* out = second ? HB : HA;
     float* zb = own ? ZH : nullptr;

@@ -517,10 +517,10 @@ __device__ __forceinline__ void layer1_run(const float* in, int ldi, const Layer
 }
 
 // The dynamics model's two hidden heads and their narrow output layers
-// (src/dynamics.py:84-91, 112-122) as ONE phase. Waves [0, NW/2) run the diff head's
-// hidden layer, waves [NW/2, NW) the log-var head's: wave w owns blocks base, base + NW/2,
-// ... with base = w (diff) or NW-1-w (log-var), which for 13 blocks per head on 8 waves
-// puts 7 / 6 / 6 / 7 blocks on the four SIMDs. Each wave then forms its split-K share of
+// (src/dynamics.py:84-91, 112-122) as ONE phase. Each wave runs one head's hidden layer
+// (pair_wave_code: waves 0, 1, 2, 7 the diff head, 3-6 the log-var head) and owns its
+// blocks base, base + NW/2, ...: 7 / 6 / 6 / 7 blocks on the four SIMDs for 13 blocks
+// per head, the 4-block wave the older one on both 7-block SIMDs. Each wave then forms its split-K share of
 // its head's output layer from exactly the columns it produced (read back from LDS by the
 // same wave: no workgroup barrier between the two layers), the output layer's fragments
 // issued before the hidden epilogue. Partials land in red slot [head][w mod NW/2], the
@@ -632,12 +632,15 @@ __device__ __forceinline__ void pair_split_heads(const float* in, int ldi, int N
                                                  float* out1, const float* Pn1, const float* P2, const float* b2,
                                                  float* out2, const float* Pn2, float* red) {
   constexpr int HW = NW / 2;
+  static_assert(NW == 8, "pair_wave_code maps 8 waves");
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool second = wave >= HW;
-  const int base = second ? NW - 1 - wave : wave;
+  const unsigned code = pair_wave_code(wave);
+  const bool second = code >> 2;
+  const int base = code & 3;
   const int NCB = (N + 15) >> 4;
   const int nc = base < NCB ? min(MAXC, (NCB - base + HW - 1) / HW) : 0;
-  float* slot = red + (size_t)((second ? HW : 0) + (second ? wave - HW : wave)) * RB * 256;
+  // head 0's slot q holds base q, head 1's slot q holds base HW - 1 - q (narrow_pair_sum's order)
+  float* slot = red + (size_t)(second ? HW + (HW - 1 - base) : base) * RB * 256;
   if (nc > 0)
     pair_split_nc<NW, RB, MAXC, NK>(nc, base, in, ldi, second ? P2 : P1, second ? b2 : b1, N, second ? out2 : out1,
                                     ldi, second ? Pn2 : Pn1, slot);
