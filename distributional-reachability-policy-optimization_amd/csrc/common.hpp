@@ -263,6 +263,46 @@ static __device__ __forceinline__ void gstore(T* p, T v) {
   *(__attribute__((address_space(1))) T*)(p) = v;
 }
 
+// An input tile [tile_rows][kpad] staged into LDS from up to three column-concatenated
+// row-major sources (torch.cat([s, a, ...], -1)); the src[0] columns optionally
+// normalised as (x - mean) / (std + 1e-6) (src/normalization.py:22-23), columns past
+// c0 + c1 + c2 zero. s0 / s1 / s2 are the sources already offset to this member; a
+// source whose columns are skipped (skip1: the action block a chain job fills from LDS)
+// may be null. Each lane issues its value, mean and std loads together from valid
+// addresses and selects afterwards: one memory round trip per element, where indexing
+// the descriptor's source array by a per-lane block index cost a pointer load plus
+// dependent value / mean / std loads (four round trips; fit staging 2.4 k cycles).
+template <int NT>
+__device__ __forceinline__ void stage_input_tile(float* xin, int ldx, int tile_rows, int nrows, int64_t row0, int kpad,
+                                                 const float* s0, const float* s1, const float* s2, int c0, int c1,
+                                                 int c2, int ld0, int ld1, int ld2, const float* nmean,
+                                                 const float* nstd, bool skip1, float* save_x, int64_t save_row0) {
+  const int din0 = c0 + c1 + c2;
+  for (int e = threadIdx.x; e < tile_rows * kpad; e += NT) {
+    const int r = e / kpad, k = e - r * kpad;
+    float v = 0.f;
+    if (r < nrows && k < din0) {
+      const int q = k < c0 ? 0 : (k - c0 < c1 ? 1 : 2);
+      const int kk = q == 0 ? k : (q == 1 ? k - c0 : k - c0 - c1);
+      const bool zero = skip1 && q == 1;
+      const bool use0 = q == 0 || zero;
+      const float* sp = use0 ? s0 : (q == 1 ? s1 : s2);
+      const int ld = use0 ? ld0 : (q == 1 ? ld1 : ld2);
+      const float x = gload(sp + (row0 + r) * ld + (zero ? 0 : kk));
+      if (nmean) {
+        const int km = q == 0 ? kk : 0;
+        const float mu = gload(nmean + km), sd = gload(nstd + km);
+        v = q == 0 ? (x - mu) / (sd + 1e-6f) : x;
+      } else {
+        v = x;
+      }
+      if (zero) v = 0.f;
+      if (save_x) gstore(save_x + (save_row0 + r) * din0 + k, v);
+    }
+    xin[r * ldx + k] = v;
+  }
+}
+
 static __device__ __forceinline__ const float* uniform_ptr(const float* p) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);

@@ -303,19 +303,9 @@ __device__ __forceinline__ void fit_fb_body(FitK& k, float* smem) {
   FSTAMP(9);
   // ---- input x = [normalize(s), a] -------------------------------------------------
   const int kpad = nk1 * 16;
-  for (int e = tid; e < FF_ROWS * kpad; e += FF_NT) {
-    const int r = e / kpad, kk = e - r * kpad;
-    float v = 0.f;
-    if (r < nrows && kk < din0) {
-      const int64_t row = row0 + r;
-      const int q = kk < c0 ? 0 : 1;
-      const int kq = q == 0 ? kk : kk - c0;
-      v = gload(F.src[q] + (size_t)z * F.sstride[q] + row * F.ld[q] + kq);
-      if (q == 0 && F.nmean) v = (v - gload(F.nmean + kq)) / (gload(F.nstd + kq) + 1e-6f);
-      if (F.save_x && tsave) gstore(F.save_x + (zr + r) * din0 + kk, v);
-    }
-    xin[r * FF_LDH + kk] = v;
-  }
+  stage_input_tile<FF_NT>(xin, FF_LDH, FF_ROWS, nrows, row0, kpad, F.src[0] + (size_t)z * F.sstride[0],
+                         c1 ? F.src[1] + (size_t)z * F.sstride[1] : nullptr, nullptr, c0, c1, 0, F.ld[0], F.ld[1], 0,
+                         F.nmean, F.nstd, false, tsave ? F.save_x : nullptr, (int64_t)zr);
   lds_barrier();
   FSTAMP(1);
 

@@ -139,28 +139,11 @@ __global__ __launch_bounds__(FW_NT) void mlp_fwd_kernel(drpo_mlp_fwd_t a) {
   const bool split = a.trunk && a.split_heads;
   const bool tsave = !split || lb.y == 0;
   STAMP(0);
-  for (int e = tid; e < FW_ROWS * kpad; e += FW_NT) {
-    const int r = e / kpad, k = e - r * kpad;
-    float v = 0.f;
-    if (r < nrows && k < din0) {
-      const int64_t row = row0 + r;
-      int kk = k;
-      const float* src;
-      if (kk < a.cols[0]) {
-        src = a.src[0] + (size_t)z * a.sstride[0] + row * a.ld[0];
-      } else if (kk - a.cols[0] < a.cols[1]) {
-        kk -= a.cols[0];
-        src = a.src[1] + (size_t)z * a.sstride[1] + row * a.ld[1];
-      } else {
-        kk -= a.cols[0] + a.cols[1];
-        src = a.src[2] + (size_t)z * a.sstride[2] + row * a.ld[2];
-      }
-      v = src[kk];
-      if (k < a.cols[0] && a.nmean) v = (v - a.nmean[kk]) / (a.nstd[kk] + 1e-6f);
-      if (a.save_x && tsave) a.save_x[((size_t)z * a.rows + row) * din0 + k] = v;
-    }
-    xin[r * LDH + k] = v;
-  }
+  stage_input_tile<FW_NT>(xin, LDH, FW_ROWS, nrows, row0, kpad, a.src[0] + (size_t)z * a.sstride[0],
+                          a.cols[1] ? a.src[1] + (size_t)z * a.sstride[1] : nullptr,
+                          a.cols[2] ? a.src[2] + (size_t)z * a.sstride[2] : nullptr, a.cols[0], a.cols[1], a.cols[2],
+                          a.ld[0], a.ld[1], a.ld[2], a.nmean, a.nstd, false, tsave ? a.save_x : nullptr,
+                          (int64_t)z * a.rows + row0);
   lds_barrier();
   STAMP(1);
   if (!a.trunk) {
@@ -422,19 +405,11 @@ __global__ __launch_bounds__(FW_NT) __attribute__((amdgpu_waves_per_eu(RB == 1 ?
   const int kpad = round_up(din0, 16);
   // chain jobs: the src[1] block (the action) comes from the pre net's head below
   const bool chain = a->pre.nl > 0;
-  for (int e = tid; e < ROWS * kpad; e += FW_NT) {
-    const int r = e / kpad, k = e - r * kpad;
-    float v = 0.f;
-    if (r < nrows && k < din0) {
-      const int64_t row = row0 + r;
-      const int q = k < c0 ? 0 : (k - c0 < c1 ? 1 : 2);
-      const int kk = q == 0 ? k : (q == 1 ? k - c0 : k - c0 - c1);
-      if (!(chain && q == 1)) v = a->src[q][(size_t)z * a->sstride[q] + row * a->ld[q] + kk];
-      if (q == 0 && a->nmean) v = (v - a->nmean[kk]) / (a->nstd[kk] + 1e-6f);
-      if (a->save_x) a->save_x[((size_t)z * a->rows + row) * din0 + k] = v;
-    }
-    xin[r * LDH + k] = v;
-  }
+  const int c2 = a->cols[2];
+  stage_input_tile<FW_NT>(xin, LDH, ROWS, nrows, row0, kpad, a->src[0] + (size_t)z * a->sstride[0],
+                          (c1 && !chain) ? a->src[1] + (size_t)z * a->sstride[1] : nullptr,
+                          c2 ? a->src[2] + (size_t)z * a->sstride[2] : nullptr, c0, c1, c2, a->ld[0], a->ld[1],
+                          a->ld[2], a->nmean, a->nstd, chain, a->save_x, (int64_t)z * a->rows + row0);
   lds_barrier();
   STAMP(1);
   if (chain) {
